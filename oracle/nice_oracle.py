@@ -1,0 +1,181 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.  Never imported by the product path.
+
+CPU restatement of NICE-SLAM's ``Renderer.render_batch_ray`` hot path, written
+as plain functions over torch CPU ops with the reference's op sequence and
+dtypes (float64 depth/coordinate chain, float32 features and decoders), so that
+autograd through it yields the reference's gradients.  Used by
+
+  * tests/ (parity checker for the HIP path, pinned against tests/golden/*.npz,
+    which tests/golden/make_golden.py captured from the reference itself), and
+  * bench.py's ``cpu_baseline`` leg (``kind: "port"``).
+
+Parity status: PINNED — tests/test_oracle_golden.py checks this module against
+the golden vectors produced by importing /root/reference in the build container.
+
+Every function cites the reference lines it restates.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+STAGE_DECODERS = {  # decoder.py:341-370 (which MLPs feed raw at each stage)
+    "coarse": ("coarse",),
+    "middle": ("middle",),
+    "fine": ("fine", "middle"),
+    "color": ("fine", "color", "middle"),
+}
+
+
+def normalize_3d_coordinate(p: torch.Tensor, bound: torch.Tensor) -> torch.Tensor:
+    """common.py:280-295 — per axis ((p-lo)/(hi-lo))*2-1 in float64."""
+    cols = [((p[:, k] - bound[k, 0]) / (bound[k, 1] - bound[k, 0])) * 2 - 1.0 for k in range(3)]
+    return torch.stack(cols, dim=1)
+
+
+def sample_grid_feature(p: torch.Tensor, grid: torch.Tensor, bound: torch.Tensor) -> torch.Tensor:
+    """decoder.py:179-188 — trilinear (mode 'bilinear' on 5-D), border padding,
+    align_corners=True.  Returns [P, C]."""
+    vgrid = normalize_3d_coordinate(p, bound).unsqueeze(0)[:, :, None, None].float()
+    c = F.grid_sample(grid, vgrid, padding_mode='border', align_corners=True, mode='bilinear')
+    return c.squeeze(-1).squeeze(-1).transpose(1, 2).squeeze(0)
+
+
+def _lin(x, prm, name):
+    return F.linear(x, prm[name + '.weight'], prm[name + '.bias'])
+
+
+def mlp_forward(p, grids, prm, pre, name, bound, color=False, concat=False):
+    """decoder.py:190-219 (MLP.forward, fourier embedding, skips=[2])."""
+    c = sample_grid_feature(p, grids['grid_' + name], bound)
+    if concat:  # decoder.py:196-202: middle feature concatenated without grad
+        with torch.no_grad():
+            c_mid = sample_grid_feature(p, grids['grid_middle'], bound)
+        c = torch.cat([c, c_mid], dim=1)
+    pf = p.float()
+    emb = torch.sin(pf @ prm[pre + 'embedder._B'])  # decoder.py:26-30
+    h = emb
+    for i in range(5):
+        h = F.relu(_lin(h, prm, f'{pre}pts_linears.{i}'))
+        h = h + _lin(c, prm, f'{pre}fc_c.{i}')
+        if i == 2:
+            h = torch.cat([emb, h], -1)
+    out = _lin(h, prm, pre + 'output_linear')
+    return out if color else out.squeeze(-1)
+
+
+def mlp_no_xyz_forward(p, grids, prm, pre, bound):
+    """decoder.py:285-297 (coarse decoder)."""
+    c = sample_grid_feature(p, grids['grid_coarse'], bound)
+    h = c
+    for i in range(5):
+        h = F.relu(_lin(h, prm, f'{pre}pts_linears.{i}'))
+        if i == 2:
+            h = torch.cat([c, h], -1)
+    return _lin(h, prm, pre + 'output_linear').squeeze(-1)
+
+
+def nice_forward(p, grids, prm, dec_bounds, stage):
+    """decoder.py:336-370 — raw [P,4]; color-decoder channel 3 is overwritten."""
+    P = p.shape[0]
+    if stage == 'coarse':
+        occ = mlp_no_xyz_forward(p, grids, prm, 'coarse_decoder.', dec_bounds['coarse'])
+        raw = torch.zeros(P, 4, dtype=torch.float32)
+        raw[..., -1] = occ
+        return raw
+    if stage == 'middle':
+        occ = mlp_forward(p, grids, prm, 'middle_decoder.', 'middle', dec_bounds['middle'])
+        raw = torch.zeros(P, 4, dtype=torch.float32)
+        raw[..., -1] = occ
+        return raw
+    fine_occ = mlp_forward(p, grids, prm, 'fine_decoder.', 'fine', dec_bounds['fine'], concat=True)
+    if stage == 'fine':
+        raw = torch.zeros(P, 4, dtype=torch.float32)
+    else:
+        raw = mlp_forward(p, grids, prm, 'color_decoder.', 'color', dec_bounds['color'], color=True)
+    mid_occ = mlp_forward(p, grids, prm, 'middle_decoder.', 'middle', dec_bounds['middle'])
+    raw[..., -1] = fine_occ + mid_occ
+    return raw
+
+
+def eval_points(p, grids, prm, bound, dec_bounds, stage):
+    """Renderer.py:36-93 — strict in-bound mask against the renderer bound,
+    out-of-bound points get raw[:,3] = 100."""
+    mask = ((p[:, 0] < bound[0][1]) & (p[:, 0] > bound[0][0]) &
+            (p[:, 1] < bound[1][1]) & (p[:, 1] > bound[1][0]) &
+            (p[:, 2] < bound[2][1]) & (p[:, 2] > bound[2][0]))
+    ret = nice_forward(p, grids, prm, dec_bounds, stage)
+    ret[~mask, 3] = 100
+    return ret
+
+
+def sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf):
+    """Renderer.py:116-224 — z_vals [N, S] float64 (stratified + surface, sorted)."""
+    N = rays_o.shape[0]
+    if gt_depth is None:
+        n_surf = 0
+        near = 0.01
+    else:
+        gt_depth = gt_depth.reshape(-1, 1)
+        near = gt_depth.repeat(1, n_strat) * 0.01
+    with torch.no_grad():
+        o = rays_o.clone().detach().unsqueeze(-1)
+        d = rays_d.clone().detach().unsqueeze(-1)
+        t = (bound.unsqueeze(0) - o) / d
+        far_bb, _ = torch.min(torch.max(t, dim=2)[0], dim=1)
+        far_bb = far_bb.unsqueeze(-1) + 0.01
+    far = torch.clamp(far_bb, 0, torch.max(gt_depth * 1.2)) if gt_depth is not None else far_bb
+    if n_surf > 0:
+        pos = gt_depth > 0
+        ts = torch.linspace(0., 1., steps=n_surf).double()
+        zs = torch.zeros(N, n_surf).double()
+        g = gt_depth[pos].unsqueeze(-1).repeat(1, n_surf)
+        zs[pos.squeeze(-1), :] = 0.95 * g * (1. - ts) + 1.05 * g * ts
+        zs[~pos.squeeze(-1), :] = 0.001 * (1. - ts) + torch.max(gt_depth) * ts
+    tv = torch.linspace(0., 1., steps=n_strat)
+    z = near * (1. - tv) + far * tv
+    if n_surf > 0:
+        z, _ = torch.sort(torch.cat([z, zs.double()], -1), -1)
+    return z
+
+
+def composite(raw, z_vals):
+    """common.py:215-256 with occupancy=True: alpha = sigmoid(10 occ), exclusive
+    cumprod of (1-alpha+1e-10); rgb, depth (f64) and depth variance (f64)."""
+    rgb = raw[..., :-1]
+    alpha = torch.sigmoid(10 * raw[..., -1])
+    ones = torch.ones((alpha.shape[0], 1), dtype=torch.float32)
+    weights = alpha.float() * torch.cumprod(torch.cat([ones, (1. - alpha + 1e-10).float()], -1), -1)[:, :-1]
+    rgb_map = torch.sum(weights[..., None] * rgb, -2)
+    depth_map = torch.sum(weights * z_vals, -1)
+    tmp = z_vals - depth_map.unsqueeze(-1)
+    depth_var = torch.sum(weights * tmp * tmp, dim=1)
+    return depth_map, depth_var, rgb_map, weights
+
+
+def render_batch_ray(grids, prm, dec_bounds, bound, rays_d, rays_o, stage, gt_depth=None,
+                     n_strat=32, n_surf=16):
+    """Renderer.py:95-262 (N_importance = 0, lindisp/perturb off, occupancy on).
+    Returns (depth f64 [N], uncertainty f64 [N], color f32 [N,3])."""
+    if stage == 'coarse':
+        gt_depth = None
+    z = sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf)
+    S = z.shape[1]
+    pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
+    raw = eval_points(pts.reshape(-1, 3), grids, prm, bound, dec_bounds, stage)
+    raw = raw.reshape(rays_o.shape[0], S, -1)
+    depth, var, color, _ = composite(raw, z)
+    return depth, var, color
+
+
+def points_for_rays(rays_o, rays_d, bound, gt_depth, stage, n_strat=32, n_surf=16):
+    """The float64 sample points render_batch_ray evaluates (Renderer.py:227-231)."""
+    if stage == 'coarse':
+        gt_depth = None
+    z = sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf)
+    return z, (rays_o[..., None, :].double() + rays_d[..., None, :].double() * z[..., :, None])
+
+
+def params_from_module(nice) -> dict:
+    """name -> tensor view of a NICE module's parameters (reference names)."""
+    return dict(nice.named_parameters())

@@ -1,0 +1,188 @@
+"""Generate golden vectors for the render hot path FROM THE REFERENCE ITSELF.
+
+Runs only in the build container, where /root/reference (WohimLee/NICE-SLAM-annotation)
+is mounted read-only.  It imports the reference's own modules
+
+    src.config.load_config / get_model   (src/config.py:10-79)
+    src.utils.Renderer.Renderer          (src/utils/Renderer.py:5-262)
+
+builds a tiny scene exactly as src/NICE_SLAM.py:188-320 does (bound snapping,
+per-decoder .bound, grid_init), renders seeded synthetic rays through
+``Renderer.render_batch_ray`` on the CPU, back-propagates random upstream
+gradients, and stores inputs / outputs / gradients as .npz fixtures next to this
+script.  Nothing of the reference is copied: only numeric vectors are written.
+
+Harness patch: decoder.py:340 builds ``'cuda:{p.get_device()}'``
+which is ``'cuda:-1'`` on the CPU; NICE.forward is re-bound to a body with the
+same stage logic that allocates on ``p.device`` instead.
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("NICE_REF", "/root/reference")
+sys.path.insert(0, os.path.join(REPO, "nice-slam-annotation_amd"))
+
+from nicecore import scene as S  # noqa: E402
+
+
+def _import_reference():
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    cwd = os.getcwd()
+    os.chdir(REF)
+    from src import config as ref_config  # noqa: F401
+    from src.utils.Renderer import Renderer as RefRenderer
+    from src.conv_onet.models import decoder as ref_decoder
+    cfg = ref_config.load_config('configs/Replica/room0.yaml', 'configs/nice_slam.yaml')
+    os.chdir(cwd)
+
+    def forward_cpu_safe(self, p, c_grid, stage='middle', **kwargs):
+        # stage semantics of decoder.py:336-370, allocating on p.device
+        dev = p.device
+        if stage in ('coarse', 'middle'):
+            dec = self.coarse_decoder if stage == 'coarse' else self.middle_decoder
+            occ = dec(p, c_grid).squeeze(0)
+            raw = torch.zeros(occ.shape[0], 4, device=dev).float()
+            raw[..., -1] = occ
+            return raw
+        fine_occ = self.fine_decoder(p, c_grid)
+        if stage == 'fine':
+            raw = torch.zeros(fine_occ.shape[0], 4, device=dev).float()
+        else:
+            raw = self.color_decoder(p, c_grid)
+        middle_occ = self.middle_decoder(p, c_grid).squeeze(0)
+        raw[..., -1] = fine_occ + middle_occ
+        return raw
+
+    ref_decoder.NICE.forward = forward_cpu_safe
+    return ref_config, RefRenderer, cfg
+
+
+CASES = [
+    # name, stage, n_rays, with_depth, zero_frac, outside_frac, seed
+    ("color_depth", "color", 24, True, 0.15, 0.25, 11),
+    ("fine_depth", "fine", 20, True, 0.1, 0.2, 12),
+    ("middle_nodepth", "middle", 20, False, 0.0, 0.25, 13),
+    ("coarse", "coarse", 16, False, 0.0, 0.25, 14),
+    ("color_nodepth", "color", 12, False, 0.0, 0.0, 15),
+    ("middle_depth", "middle", 16, True, 0.2, 0.0, 16),
+]
+
+
+def main():
+    ref_config, RefRenderer, cfg = _import_reference()
+    scene = S.make_scene("tiny")
+    cfg['mapping']['bound'] = S.PRESETS["tiny"]["bound"]
+    torch.manual_seed(0)
+    model = ref_config.get_model(cfg, nice=True)
+    # load_bound (src/NICE_SLAM.py:188-208), reproduced by the reference formula
+    bound = torch.from_numpy(np.array(cfg['mapping']['bound']) * cfg['scale'])
+    bd = cfg['grid_len']['bound_divisible']
+    bound[:, 1] = (((bound[:, 1] - bound[:, 0]) / bd).int() + 1) * bd + bound[:, 0]
+    assert torch.equal(bound, scene.bound), (bound, scene.bound)
+    model.bound = bound
+    for n in ("middle", "fine", "color"):
+        getattr(model, n + "_decoder").bound = bound
+    model.coarse_decoder.bound = bound * cfg['model']['coarse_bound_enlarge']
+
+    gen = torch.Generator().manual_seed(5)
+    grids = S.init_grids(scene.shapes, generator=gen)
+    # Random-init decoders give occ ~ 0, i.e. alpha ~ 0.5 on every sample, so all
+    # compositing weight would sit on the first samples and later samples would be
+    # untested.  Scale the grids up and bias the occupancy heads negative so the
+    # transmittance survives along the ray (weights spread over all samples).
+    scale = {'grid_coarse': 30.0, 'grid_middle': 30.0, 'grid_fine': 3000.0, 'grid_color': 30.0}
+    grids_big = {k: (v * scale[k]).contiguous() for k, v in grids.items()}
+    with torch.no_grad():
+        model.coarse_decoder.output_linear.bias.fill_(-0.7)
+        model.middle_decoder.output_linear.bias.fill_(-0.55)
+        model.fine_decoder.output_linear.bias.fill_(-0.5)
+
+    slam = types.SimpleNamespace(nice=True, bound=bound, H=scene.H, W=scene.W, fx=scene.fx,
+                                 fy=scene.fy, cx=scene.cx, cy=scene.cy)
+    renderer = RefRenderer(cfg, None, slam)
+
+    sc = {
+        "bound": bound.numpy(),
+        "coarse_bound": model.coarse_decoder.bound.numpy(),
+        **{k: v.numpy() for k, v in grids_big.items()},
+        **{"param/" + n: p.detach().numpy() for n, p in model.named_parameters()},
+    }
+    np.savez_compressed(os.path.join(HERE, "scene_tiny.npz"), **sc)
+    meta = {"scene": "tiny", "shapes": scene.shapes, "cases": [], "torch": torch.__version__,
+            "reference": "WohimLee/NICE-SLAM-annotation (read-only mount)",
+            "n_samples": cfg['rendering']['N_samples'], "n_surface": cfg['rendering']['N_surface']}
+
+    for name, stage, n, with_depth, zf, of, seed in CASES:
+        ro, rd, dep, col = S.synth_rays(scene, n, n_poses=6, seed=seed,
+                                        zero_depth_frac=zf, outside_frac=of)
+        ro = ro.clone().requires_grad_(True)
+        rd = rd.clone().requires_grad_(True)
+        g = {k: v.clone().requires_grad_(True) for k, v in grids_big.items()}
+        for p in model.parameters():
+            p.grad = None
+        gt = dep if with_depth else None
+        seen = {}
+        orig_eval = renderer.eval_points
+
+        def recording_eval(p, decoders, c=None, stage='color', device='cuda:0'):
+            seen["pts"] = p.detach().clone()
+            return orig_eval(p, decoders, c, stage, device)
+
+        renderer.eval_points = recording_eval
+        depth, var, color = renderer.render_batch_ray(g, model, rd, ro, 'cpu', stage, gt)
+        renderer.eval_points = orig_eval
+        gen2 = torch.Generator().manual_seed(seed + 100)
+        gd = torch.randn(depth.shape, generator=gen2, dtype=torch.float64)
+        gv = torch.randn(var.shape, generator=gen2, dtype=torch.float64) * 0.5
+        gc = torch.randn(color.shape, generator=gen2, dtype=torch.float32)
+        torch.autograd.backward([depth, var, color], [gd, gv, gc])
+        rec = {
+            "rays_o": ro.detach().numpy(), "rays_d": rd.detach().numpy(),
+            "gt_depth": dep.numpy(), "gt_color": col.numpy(),
+            "depth": depth.detach().numpy(), "var": var.detach().numpy(),
+            "color": color.detach().numpy(),
+            "g_depth": gd.numpy(), "g_var": gv.numpy(), "g_color": gc.numpy(),
+            "grad/rays_o": ro.grad.numpy(), "grad/rays_d": rd.grad.numpy(),
+        }
+        for k, v in g.items():
+            if v.grad is not None:
+                rec["grad/" + k] = v.grad.numpy()
+        for pn, p in model.named_parameters():
+            if p.grad is not None:
+                rec["grad/param/" + pn] = p.grad.numpy()
+        # eval_points on the same sample points (Renderer.py:36-93), no grad
+        pts = seen["pts"]
+        with torch.no_grad():
+            raw = renderer.eval_points(pts, model, g, stage, 'cpu')
+        rec["pts"] = pts.numpy()
+        rec["raw"] = raw.numpy()
+        np.savez_compressed(os.path.join(HERE, f"case_{name}.npz"), **rec)
+        meta["cases"].append(dict(name=name, stage=stage, n_rays=n, with_depth=with_depth))
+        with torch.no_grad():
+            from nicecore.scene import linspace_tables  # noqa: F401
+            occ = raw[:, 3].reshape(n, -1)
+            a = torch.sigmoid(10 * occ)
+            T = torch.cumprod(torch.cat([torch.ones(n, 1), 1 - a + 1e-10], 1), 1)[:, :-1]
+            w = a * T
+            print(f"  alpha mean {a.mean():.3f}  T_end mean {T[:, -1].mean():.3f}  "
+                  f"w.max/ray mean {w.max(1)[0].mean():.3f}  frac samples w>1e-3 {(w > 1e-3).float().mean():.3f}")
+        print(f"{name}: depth[:3]={depth[:3].tolist()} |g_grid| keys={[k for k in rec if k.startswith('grad/grid')]}")
+    with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

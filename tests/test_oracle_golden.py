@@ -1,0 +1,61 @@
+"""The CPU oracle (oracle/nice_oracle.py) against golden vectors captured from the
+reference renderer (tests/golden/make_golden.py).  Pins the oracle."""
+import pytest
+import torch
+
+from conftest import CASE_NAMES, load_case, load_meta, load_scene
+from oracle import nice_oracle as O
+
+
+def _run(case, grids_req=True):
+    meta = load_meta()
+    stage = next(c for c in meta["cases"] if c["name"] == case)["stage"]
+    bound, cbound, grids, params = load_scene()
+    rec = load_case(case)
+    ro = rec["rays_o"].clone().requires_grad_(True)
+    rd = rec["rays_d"].clone().requires_grad_(True)
+    g = {k: v.clone().requires_grad_(grids_req) for k, v in grids.items()}
+    prm = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    with_depth = next(c for c in meta["cases"] if c["name"] == case)["with_depth"]
+    gt = rec["gt_depth"] if with_depth else None
+    dec_bounds = {"coarse": cbound, "middle": bound, "fine": bound, "color": bound}
+    depth, var, color = O.render_batch_ray(g, prm, dec_bounds, bound, rd, ro, stage, gt,
+                                           meta["n_samples"], meta["n_surface"])
+    torch.autograd.backward([depth, var, color], [rec["g_depth"], rec["g_var"], rec["g_color"]])
+    return rec, (depth, var, color), ro, rd, g, prm, stage, bound, dec_bounds, gt
+
+
+@pytest.mark.parametrize("case", CASE_NAMES)
+def test_oracle_outputs_and_grads(case):
+    rec, (depth, var, color), ro, rd, g, prm, *_ = _run(case)
+    # same torch CPU ops, same order -> bitwise or last-ulp equal
+    torch.testing.assert_close(depth.detach(), rec["depth"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(var.detach(), rec["var"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(color.detach(), rec["color"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(ro.grad, rec["grad/rays_o"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rd.grad, rec["grad/rays_d"], rtol=1e-5, atol=1e-6)
+    for k, v in g.items():
+        key = "grad/" + k
+        if key in rec:
+            torch.testing.assert_close(v.grad, rec[key], rtol=1e-5, atol=1e-7)
+        else:
+            assert v.grad is None or float(v.grad.abs().max()) == 0.0
+    for k, v in prm.items():
+        key = "grad/param/" + k
+        if key in rec:
+            torch.testing.assert_close(v.grad, rec[key], rtol=1e-5, atol=1e-6)
+        else:
+            assert v.grad is None or float(v.grad.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("case", CASE_NAMES)
+def test_oracle_sample_points_and_raw(case):
+    meta = load_meta()
+    rec, _, ro, rd, g, prm, stage, bound, dec_bounds, gt = _run(case)
+    z, pts = O.points_for_rays(rec["rays_o"], rec["rays_d"], bound, gt, stage,
+                               meta["n_samples"], meta["n_surface"])
+    assert torch.equal(pts.reshape(-1, 3), rec["pts"])  # float64 chain is exact
+    with torch.no_grad():
+        raw = O.eval_points(rec["pts"], {k: v.detach() for k, v in g.items()},
+                            {k: v.detach() for k, v in prm.items()}, bound, dec_bounds, stage)
+    torch.testing.assert_close(raw, rec["raw"], rtol=0, atol=0)
