@@ -1,0 +1,266 @@
+"""Benchmark: rendered rays/s (fwd+bwd) of NICE-SLAM's render_batch_ray hot path.
+
+Workload (BASELINE.json configs[1]): Replica room0 scene (snapped bound, grid
+shapes middle [21,28,37], fine/color [43,56,74]), 1000 rays x 48 samples per GPU
+(32 stratified + 16 surface), stage 'color' (middle + fine + color decoders),
+mapper/BA gradients (rays, the three grids and every decoder parameter), the
+mapper's L1 loss (src/Mapper.py:603-612) and backward.  Synthetic seeded rays and
+random-init decoders / N(0,.) grids (no datasets or checkpoints exist here).
+
+One step = render_batch_ray + loss + backward (+ for N>1 the RCCL all-reduce of
+grid and decoder gradients, and the all-reduce(MAX) of the batch-global depth
+bound that render_batch_ray needs before sampling).  Weak scaling: every rank
+renders its own 1000 rays.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ba|tracker]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "nice-slam-annotation_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+METRIC = "rendered rays/sec (fwd+bwd), Replica room0 1000 rays×48 samples, 1/2/4/8 GPU"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
+HBM_PEAK_GBS = 8000.0
+MAC = {"coarse": 6176, "middle": 15479, "fine": 20599, "color": 15575}  # per point
+TRI_FLOP = 8 * 32 * 2  # one trilinear lookup of 32 channels
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rays", type=int, default=1000)
+    ap.add_argument("--scene", default="replica_room0")
+    ap.add_argument("--stage", default="color")
+    ap.add_argument("--mode", default="ba", choices=["ba", "tracker"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="bounded CPU-oracle sample (0 disables)")
+    ap.add_argument("--layout", default="channels_last", choices=["channels_last", "ncdhw"])
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def build_workload(args, rank, device):
+    from nicecore import decoder as D
+    from nicecore import scene as S
+    from nicecore.renderer import Renderer
+    sc = S.make_scene(args.scene)
+    gen = torch.Generator().manual_seed(0)
+    grids = S.init_grids(sc.shapes, generator=gen, device=device,
+                         channels_last=(args.layout == "channels_last"))
+    model = D.build_default_nice(seed=0).to(device)
+    model.bound = sc.bound.to(device)
+    for n in ("middle", "fine", "color"):
+        getattr(model, n + "_decoder").bound = model.bound
+    model.coarse_decoder.bound = (sc.bound * 2).to(device)
+    ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000 + rank)
+    slam = types.SimpleNamespace(nice=True, bound=sc.bound, H=sc.H, W=sc.W, fx=sc.fx, fy=sc.fy,
+                                 cx=sc.cx, cy=sc.cy)
+    cfg = {"rendering": dict(S.DEFAULT_RENDERING), "scale": 1, "occupancy": True}
+    renderer = Renderer(cfg, None, slam)
+    ba = args.mode == "ba"
+    for g in grids.values():
+        g.requires_grad_(ba)
+    for p in model.parameters():
+        p.requires_grad_(ba)
+    w = dict(sc=sc, grids=grids, model=model, renderer=renderer,
+             ro=ro.to(device).requires_grad_(True), rd=rd.to(device).requires_grad_(True),
+             gt=dep.to(device), gtc=col.to(device), ba=ba)
+    return w
+
+
+def make_step(w, args, world, device):
+    import torch.distributed as dist
+    grids, model, renderer = w["grids"], w["model"], w["renderer"]
+    ro, rd, gt, gtc = w["ro"], w["rd"], w["gt"], w["gtc"]
+    params = [p for p in model.parameters() if p.requires_grad]
+    gvals = [g for g in grids.values() if g.requires_grad]
+    depth_mask = (gt > 0).double()
+
+    def step():
+        for t in params + gvals + [ro, rd]:
+            t.grad = None
+        dmax = None
+        if world > 1:  # Renderer.py:157/:194 use max(gt_depth) over the whole (sharded) batch
+            dmax = gt.max().reshape(1)
+            dist.all_reduce(dmax, op=dist.ReduceOp.MAX)
+        depth, unc, color = renderer.render_batch_ray(grids, model, rd, ro, device, args.stage,
+                                                      gt, depth_max=dmax)
+        # src/Mapper.py:603-612 (mask applied multiplicatively: same gradient, no host sync)
+        loss = ((gt.double() - depth).abs() * depth_mask).sum()
+        if args.stage == "color":
+            loss = loss + 0.2 * (gtc - color).abs().sum()
+        loss.backward()
+        if world > 1 and w["ba"]:
+            hs = [dist.all_reduce(t.grad, async_op=True) for t in gvals + params if t.grad is not None]
+            for h in hs:
+                h.wait()
+        return loss
+    return step
+
+
+def algorithmic_flops_per_ray(stage, S, mode):
+    decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
+            "color": ["fine", "middle", "color"]}[stage]
+    lk_fwd = {"coarse": 1, "middle": 1, "fine": 3, "color": 4}[stage]
+    lk_grad = {"coarse": 1, "middle": 1, "fine": 2, "color": 3}[stage]
+    macs = sum(MAC[d] for d in decs)
+    fwd = 2 * macs + TRI_FLOP * lk_fwd
+    bwd = 2 * macs + 2 * TRI_FLOP * lk_grad + (2 * macs if mode == "ba" else 0)
+    return fwd * S, bwd * S
+
+
+def cpu_baseline(args, seconds):
+    """The CPU oracle (torch-CPU restatement of the reference path) on a bounded sample."""
+    from oracle import nice_oracle as O
+    from nicecore import decoder as D
+    from nicecore import scene as S
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    torch.set_num_threads(threads)
+    sc = S.make_scene(args.scene)
+    grids = S.init_grids(sc.shapes, generator=torch.Generator().manual_seed(0))
+    m = D.build_default_nice(seed=0)
+    prm = {k: v.detach().clone().requires_grad_(args.mode == "ba") for k, v in m.named_parameters()}
+    g = {k: v.requires_grad_(args.mode == "ba") for k, v in grids.items()}
+    dec_b = S.decoder_bounds(sc.bound)
+    ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000)
+    mask = (dep > 0).double()
+
+    def it():
+        for t in list(prm.values()) + list(g.values()):
+            t.grad = None
+        ro_ = ro.clone().requires_grad_(True)
+        rd_ = rd.clone().requires_grad_(True)
+        d, u, c = O.render_batch_ray(g, prm, dec_b, sc.bound, rd_, ro_, args.stage, dep)
+        loss = ((dep.double() - d).abs() * mask).sum() + 0.2 * (col - c).abs().sum()
+        loss.backward()
+
+    it()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        it()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    return {"value": args.rays * n / el, "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{n} iterations x {args.rays} rays x 48 samples, stage {args.stage}, "
+                      f"{args.mode} grads, torch CPU fp32/fp64 oracle, {threads} threads"}
+
+
+def read_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc
+    summary (profiles/*traffic*.json), if present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*traffic*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    device = torch.device("cuda", torch.cuda.current_device())
+    from nicecore import _lib as L
+    L.load()
+    w = build_workload(args, rank, device)
+    step = make_step(w, args, world, device)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-kernel breakdown (separate pass, all kernels event-timed) -> dominant kernel
+    with L.KernelTimer() as kt_all:
+        for _ in range(max(3, min(args.steps, 10))):
+            step()
+    torch.cuda.synchronize()
+    breakdown = {k: ms / n for k, (ms, n) in kt_all.result.items()}
+    dominant = max(breakdown, key=breakdown.get)
+
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    with L.KernelTimer([dominant]) as kt:  # 2 event records per step, on the launch stream
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    ms_dom, n_dom = kt.result.get(dominant, (0.0, 0))
+    avg_ms = ms_dom / max(n_dom, 1)
+
+    S = 48
+    fwd_fl, bwd_fl = algorithmic_flops_per_ray(args.stage, S, args.mode)
+    per_launch = {"k_mlp_fwd": fwd_fl * args.rays, "k_mlp_bwd": bwd_fl * args.rays}
+    fl = per_launch.get(dominant)
+    roof = None
+    if fl is not None and avg_ms > 0:
+        ach = fl / (avg_ms * 1e-3) / 1e12
+        tr = read_traffic()
+        roof = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 3),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": (tr or {}).get(dominant), "avg_launch_ms": round(avg_ms, 4),
+                "flop_per_launch": fl}
+
+    value = world * args.rays * args.steps / dt
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"{args.scene} {args.rays} rays x {S} samples per GPU, stage {args.stage}, "
+                               f"{'mapper/BA grads (rays+grids+decoders)' if args.mode == 'ba' else 'tracker grads (rays)'}",
+                   "rays_per_gpu": args.rays, "samples_per_ray": S, "stage": args.stage,
+                   "mode": args.mode, "grid_layout": args.layout, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "kernels_ms": {k: round(v, 4) for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1])},
+    }
+    if world == 1 and rank == 0 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,450 @@
+// nc_abi.hip — extern "C" entry points of libnicecore.so (see include/nicecore.h).
+//
+// Plans the launches of one render_batch_ray forward / backward:
+//   forward : [k_depth_max] -> k_ray_setup -> k_mlp_fwd (all decoders of the
+//             stage in one launch) -> k_composite_fwd
+//   backward: k_composite_bwd -> k_mlp_bwd -> [k_param_reduce] -> [k_ray_grads]
+// Everything is enqueued on the caller's stream; no host synchronisation, no
+// device allocation (graph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nc_device.h"
+#include "nc_internal.h"
+
+using namespace nc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int check_hip(int e, const char* what) {
+  if (e != (int)hipSuccess) return fail(-4, std::string(what) + ": " + hipGetErrorString((hipError_t)e));
+  return 0;
+}
+
+// ---- optional per-kernel event timing (nc_timing_start / nc_timing_stop) ----
+enum KernelId {
+  KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_BWD,
+  KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_COUNT
+};
+const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
+                                       "k_composite_bwd", "k_mlp_bwd", "k_param_reduce", "k_ray_grads",
+                                       "k_points_assemble", "k_points_split_grad", "k_points_grads"};
+struct TimedLaunch {
+  hipEvent_t b, e;
+  int id;
+};
+struct Timing {
+  uint32_t mask = 0;
+  std::vector<TimedLaunch> used;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+} g_timing;
+
+template <typename F>
+int timed(int id, hipStream_t s, F&& launch) {
+  if (!(g_timing.mask & (1u << id))) return launch();
+  std::pair<hipEvent_t, hipEvent_t> ev;
+  if (!g_timing.pool.empty()) {
+    ev = g_timing.pool.back();
+    g_timing.pool.pop_back();
+  } else {
+    if (hipEventCreate(&ev.first) != hipSuccess || hipEventCreate(&ev.second) != hipSuccess) return launch();
+  }
+  (void)hipEventRecord(ev.first, s);
+  const int rc = launch();
+  (void)hipEventRecord(ev.second, s);
+  g_timing.used.push_back({ev.first, ev.second, id});
+  return rc;
+}
+
+int cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Plan {
+  int n_jobs = 0;
+  Job jobs[MAX_JOBS];
+  int occ_a = -1, occ_b = -1;
+  bool has_rgb = false;
+};
+
+// decoder.py:341-370: which decoders a stage evaluates
+int plan_stage(int stage, Plan& pl) {
+  pl = Plan();
+  auto add = [&](int kind) {
+    Job& j = pl.jobs[pl.n_jobs];
+    std::memset(&j, 0, sizeof(j));
+    j.kind = kind;
+    j.slot = pl.n_jobs;
+    pl.n_jobs++;
+  };
+  switch (stage) {
+    case NC_STAGE_COARSE: add(K_COARSE); pl.occ_a = 0; break;
+    case NC_STAGE_MIDDLE: add(K_MID); pl.occ_a = 0; break;
+    case NC_STAGE_FINE: add(K_FINE); add(K_MID); pl.occ_a = 0; pl.occ_b = 1; break;
+    case NC_STAGE_COLOR: add(K_FINE); add(K_MID); add(K_COLOR); pl.occ_a = 0; pl.occ_b = 1; pl.has_rgb = true; break;
+    default: return fail(-1, "nicecore: unknown stage " + std::to_string(stage));
+  }
+  return 0;
+}
+
+int check_grid(const nc_grid& g, const char* name) {
+  if (!g.data) return fail(-1, std::string("nicecore: grid ") + name + " is required by this stage but NULL");
+  for (int k = 0; k < 3; ++k)
+    if (g.dims[k] < 1) return fail(-1, std::string("nicecore: grid ") + name + " has an empty dimension");
+  return 0;
+}
+
+int check_dec(const nc_decoder_params& d, int kind) {
+  const bool xyz = kind != K_COARSE;
+  for (int i = 0; i < 5; ++i)
+    if (!d.lin_w[i] || !d.lin_b[i] || (xyz && (!d.fc_w[i] || !d.fc_b[i])))
+      return fail(-1, "nicecore: decoder " + std::to_string(kind) + " has a NULL parameter pointer");
+  if (!d.out_w || !d.out_b || (xyz && !d.fourier_B))
+    return fail(-1, "nicecore: decoder " + std::to_string(kind) + " has a NULL parameter pointer");
+  return 0;
+}
+
+const char* grid_name(int k) {
+  static const char* n[4] = {"grid_coarse", "grid_middle", "grid_fine", "grid_color"};
+  return n[k];
+}
+
+int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* dec) {
+  for (int j = 0; j < pl.n_jobs; ++j) {
+    const int k = pl.jobs[j].kind;
+    if (int e = check_grid(grids[k], grid_name(k))) return e;
+    if (k == K_FINE)
+      if (int e = check_grid(grids[K_MID], grid_name(K_MID))) return e;
+    if (int e = check_dec(dec[k], k)) return e;
+  }
+  return 0;
+}
+
+struct Ws {
+  size_t dmax = 0, z = 0, pts = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, total = 0;
+  int slab_wgs = 1;
+  int64_t slab_stride = 0;
+};
+
+void layout(int64_t N, int64_t P, const Plan& pl, bool rays, Ws& w) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align256(off + bytes);
+    return o;
+  };
+  w.dmax = take(16);
+  w.z = rays ? take((size_t)P * 8) : 0;
+  w.pts = rays ? take((size_t)P * 24) : 0;
+  w.occ = take((size_t)pl.n_jobs * P * 4);
+  w.rgb = take((size_t)P * 12);
+  w.gocc = take((size_t)P * 4);
+  w.grgb = take((size_t)P * 12);
+  w.dpts = take((size_t)pl.n_jobs * P * 24);
+  const int64_t blocks = (P + 63) / 64;
+  int per_job = (cu_count() + pl.n_jobs - 1) / pl.n_jobs;
+  if (per_job < 1) per_job = 1;
+  w.slab_wgs = (int)((blocks < per_job) ? (blocks > 0 ? blocks : 1) : per_job);
+  w.slab_stride = (max_param_count() + 63) & ~int64_t(63);
+  w.slab = take((size_t)pl.n_jobs * w.slab_wgs * w.slab_stride * 4);
+  w.total = off;
+  (void)N;
+}
+
+template <typename T>
+T* at(void* ws, size_t off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(ws) + off);
+}
+
+void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const nc_decoder_params* dec,
+              const double* pts, void* ws, const Ws& w, bool need_coord) {
+  std::memset(&m, 0, sizeof(m));
+  m.P = P;
+  m.n_jobs = pl.n_jobs;
+  m.slab_wgs = w.slab_wgs;
+  m.slab_stride = w.slab_stride;
+  for (int j = 0; j < pl.n_jobs; ++j) {
+    m.jobs[j] = pl.jobs[j];
+    const int k = pl.jobs[j].kind;
+    m.jobs[j].need_dw = dec[k].grad != nullptr;
+    m.jobs[j].need_grid = grids[k].grad != nullptr;
+    m.jobs[j].need_coord = need_coord;
+  }
+  std::memcpy(m.grids, grids, sizeof(m.grids));
+  std::memcpy(m.dec, dec, sizeof(m.dec));
+  m.pts = pts;
+  m.occ = at<float>(ws, w.occ);
+  m.rgb = at<float>(ws, w.rgb);
+  m.gocc = at<float>(ws, w.gocc);
+  m.grgb = at<float>(ws, w.grgb);
+  m.dpts = at<double>(ws, w.dpts);
+  m.slab = at<float>(ws, w.slab);
+}
+
+int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (int e = plan_stage(a->stage, pl)) return e;
+  if (a->n_rays < 0) return fail(-1, "nicecore: n_rays < 0");
+  if (a->n_strat < 1 || a->n_surf < 0 || a->n_surf > NC_MAX_SURF || a->n_strat + a->n_surf > NC_MAX_SAMPLES)
+    return fail(-1, "nicecore: need 1 <= N_samples, 0 <= N_surface <= 32, N_samples + N_surface <= 64");
+  if (a->n_surf > 0 && !a->gt_depth) return fail(-1, "nicecore: N_surface > 0 requires gt_depth");
+  if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
+  S = a->n_strat + a->n_surf;
+  P = a->n_rays * S;
+  layout(a->n_rays, P, pl, true, w);
+  return 0;
+}
+
+void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, const Ws& w, int64_t P, int S) {
+  std::memset(&c, 0, sizeof(c));
+  c.N = a->n_rays;
+  c.P = P;
+  c.S = S;
+  c.n_strat = a->n_strat;
+  c.n_surf = a->n_surf;
+  c.stage = a->stage;
+  c.occ_a = pl.occ_a;
+  c.occ_b = pl.occ_b;
+  c.has_rgb = pl.has_rgb;
+  c.n_jobs = pl.n_jobs;
+  c.rays_o = a->rays_o;
+  c.rays_d = a->rays_d;
+  c.gt_depth = a->gt_depth;
+  c.depth_max = a->depth_max ? a->depth_max : at<float>(ws, w.dmax);
+  std::memcpy(c.bound, a->bound, sizeof(c.bound));
+  std::memcpy(c.t_strat, a->t_strat, sizeof(c.t_strat));
+  std::memcpy(c.t_surf, a->t_surf, sizeof(c.t_surf));
+  c.z = at<double>(ws, w.z);
+  c.pts = at<double>(ws, w.pts);
+  c.occ = at<float>(ws, w.occ);
+  c.rgb = at<float>(ws, w.rgb);
+  c.depth = a->depth;
+  c.var = a->var;
+  c.color = a->color;
+  c.g_depth = a->g_depth;
+  c.g_var = a->g_var;
+  c.g_color = a->g_color;
+  c.gocc = at<float>(ws, w.gocc);
+  c.grgb = at<float>(ws, w.grgb);
+  c.dpts = at<double>(ws, w.dpts);
+  c.g_rays_o = a->g_rays_o;
+  c.g_rays_d = a->g_rays_d;
+}
+
+int fwd_grid_x(int64_t P, int n_jobs) {
+  const int64_t per = FWD_THREADS / 64 * 16;
+  const int64_t blocks = (P + per - 1) / per;
+  int x = (cu_count() + n_jobs - 1) / n_jobs;
+  if (blocks < x) x = (int)(blocks > 0 ? blocks : 1);
+  return x;
+}
+
+int64_t nparam_of(int kind) {
+  switch (kind) {
+    case K_COARSE: return Net<K_COARSE>::NPARAM;
+    case K_MID: return Net<K_MID>::NPARAM;
+    case K_FINE: return Net<K_FINE>::NPARAM;
+    case K_COLOR: return Net<K_COLOR>::NPARAM;
+  }
+  return -1;
+}
+
+int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s) {
+  ParamReduceCtx r;
+  std::memset(&r, 0, sizeof(r));
+  r.n_jobs = m.n_jobs;
+  r.slab_wgs = m.slab_wgs;
+  r.slab_stride = m.slab_stride;
+  r.slab = m.slab;
+  bool any = false;
+  for (int j = 0; j < m.n_jobs; ++j) {
+    r.jobs[j] = m.jobs[j];
+    r.grad[j] = dec[m.jobs[j].kind].grad;
+    r.nparam[j] = nparam_of(m.jobs[j].kind);
+    any |= (r.grad[j] != nullptr);
+  }
+  if (!any) return 0;
+  return check_hip(timed(KID_PARAM_REDUCE, s, [&] { return launch_param_reduce(r, max_param_count(), s); }), "k_param_reduce");
+}
+
+}  // namespace
+
+extern "C" {
+
+int nc_abi_version(void) { return NC_ABI_VERSION; }
+
+const char* nc_last_error(void) { return g_err.c_str(); }
+
+int64_t nc_param_count(int decoder) { return nparam_of(decoder); }
+
+int nc_timing_start(uint32_t kernel_mask) {
+  for (auto& t : g_timing.used) g_timing.pool.push_back({t.b, t.e});
+  g_timing.used.clear();
+  g_timing.mask = kernel_mask;
+  return 0;
+}
+
+int nc_timing_stop(double* total_ms, int64_t* launches, int max_kernels) {
+  g_timing.mask = 0;
+  for (int k = 0; k < max_kernels; ++k) {
+    if (total_ms) total_ms[k] = 0.0;
+    if (launches) launches[k] = 0;
+  }
+  for (auto& t : g_timing.used) {
+    if (hipEventSynchronize(t.e) != hipSuccess) return fail(-4, "nc_timing_stop: event sync failed");
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, t.b, t.e);
+    if (t.id < max_kernels) {
+      if (total_ms) total_ms[t.id] += ms;
+      if (launches) launches[t.id] += 1;
+    }
+    g_timing.pool.push_back({t.b, t.e});
+  }
+  g_timing.used.clear();
+  return KID_COUNT;
+}
+
+const char* nc_kernel_name(int id) { return (id >= 0 && id < KID_COUNT) ? kKernelNames[id] : ""; }
+
+size_t nc_struct_size(int which) {
+  switch (which) {
+    case 0: return sizeof(nc_render_args);
+    case 1: return sizeof(nc_points_args);
+    case 2: return sizeof(nc_grid);
+    case 3: return sizeof(nc_decoder_params);
+  }
+  return 0;
+}
+
+size_t nc_render_workspace_bytes(const nc_render_args* a) {
+  Plan pl;
+  Ws w;
+  int64_t P;
+  int S;
+  if (render_prepare(a, pl, w, P, S)) return 0;
+  return w.total;
+}
+
+int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* stream) {
+  Plan pl;
+  Ws w;
+  int64_t P;
+  int S;
+  if (int e = render_prepare(a, pl, w, P, S)) return e;
+  if (int e = check_models(pl, a->grids, a->dec)) return e;
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_rays == 0) return 0;
+  if (!a->rays_o || !a->rays_d || !a->depth || !a->var || !a->color)
+    return fail(-1, "nicecore: NULL ray input or output pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a->gt_depth && !a->depth_max)
+    if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) return e;
+  RayCtx rc;
+  fill_ray(rc, a, pl, ws, w, P, S);
+  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
+  MlpCtx m;
+  fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
+  if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(P, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
+  if (int e = check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd")) return e;
+  return 0;
+}
+
+int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void* stream) {
+  Plan pl;
+  Ws w;
+  int64_t P;
+  int S;
+  if (int e = render_prepare(a, pl, w, P, S)) return e;
+  if (int e = check_models(pl, a->grids, a->dec)) return e;
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_rays == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  RayCtx rc;
+  fill_ray(rc, a, pl, ws, w, P, S);
+  const bool need_coord = a->g_rays_o || a->g_rays_d;
+  MlpCtx m;
+  fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, need_coord);
+  bool any = need_coord;
+  for (int j = 0; j < m.n_jobs; ++j) any |= m.jobs[j].need_dw || m.jobs[j].need_grid;
+  if (!any) return 0;
+  if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
+  if (int e = check_hip(timed(KID_MLP_BWD, s, [&] { return launch_mlp_bwd(m, s); }), "k_mlp_bwd")) return e;
+  if (int e = reduce_params(m, a->dec, s)) return e;
+  if (need_coord)
+    if (int e = check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(rc, s); }), "k_ray_grads")) return e;
+  return 0;
+}
+
+static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (int e = plan_stage(a->stage, pl)) return e;
+  if (a->n_points < 0) return fail(-1, "nicecore: n_points < 0");
+  layout(0, a->n_points, pl, false, w);
+  return 0;
+}
+
+size_t nc_points_workspace_bytes(const nc_points_args* a) {
+  Plan pl;
+  Ws w;
+  if (points_prepare(a, pl, w)) return 0;
+  return w.total;
+}
+
+int nc_points_forward(const nc_points_args* a, void* ws, size_t ws_bytes, void* stream) {
+  Plan pl;
+  Ws w;
+  if (int e = points_prepare(a, pl, w)) return e;
+  if (int e = check_models(pl, a->grids, a->dec)) return e;
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_points == 0) return 0;
+  if (!a->pts || !a->raw) return fail(-1, "nicecore: NULL points input or raw output");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  MlpCtx m;
+  fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, false);
+  if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(a->n_points, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
+  return check_hip(timed(KID_POINTS_ASSEMBLE, s, [&] { return launch_points_assemble(m, a->stage, a->raw, s); }), "k_points_assemble");
+}
+
+int nc_points_backward(const nc_points_args* a, void* ws, size_t ws_bytes, void* stream) {
+  Plan pl;
+  Ws w;
+  if (int e = points_prepare(a, pl, w)) return e;
+  if (int e = check_models(pl, a->grids, a->dec)) return e;
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_points == 0) return 0;
+  if (!a->pts || !a->g_raw) return fail(-1, "nicecore: NULL points input or upstream gradient");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  MlpCtx m;
+  fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, a->g_pts != nullptr);
+  if (int e = check_hip(timed(KID_POINTS_SPLIT, s, [&] { return launch_points_split_grad(m, a->stage, a->g_raw, (float*)m.gocc, (float*)m.grgb, s); }), "k_points_split_grad"))
+    return e;
+  if (int e = check_hip(timed(KID_MLP_BWD, s, [&] { return launch_mlp_bwd(m, s); }), "k_mlp_bwd")) return e;
+  if (int e = reduce_params(m, a->dec, s)) return e;
+  if (a->g_pts)
+    if (int e = check_hip(timed(KID_POINTS_GRADS, s, [&] { return launch_points_grads(m, a->g_pts, s); }), "k_points_grads")) return e;
+  return 0;
+}
+
+}  // extern "C"

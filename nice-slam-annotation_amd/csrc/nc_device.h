@@ -1,0 +1,203 @@
+// nc_device.h — device-side building blocks of the NICE render core (gfx950).
+//
+// Register layout used by every point-batched MLP in this library ("C layout"):
+// a wavefront owns 16 points; lane l handles point i = l & 15 and lane-group
+// g = l >> 4 (0..3).  A feature vector of width 16*T is spread over the four
+// lanes of a point: register 4*t + r of lane (i, g) holds feature 16*t + 4*g + r.
+// This is exactly the accumulator layout of v_mfma_f32_16x16x4_f32 when the MFMA
+// computes Y^T = W * X^T with the point on the MFMA column, so a layer's output
+// feeds the next layer's B operand with no data movement (k-step s of the next
+// layer uses register s).  Weights are the A operand, read from LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nicecore.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace nc {
+
+constexpr int HID = 32;    // hidden width of every NICE decoder (decoder.py:316)
+constexpr int EMB = 93;    // Fourier mapping size (decoder.py:137)
+constexpr int EMBP = 96;   // padded to 16
+constexpr int NSTEP_H = 8; // k-steps of a 32-wide input (4 features per step)
+
+enum Kind { K_COARSE = NC_DEC_COARSE, K_MID = NC_DEC_MIDDLE, K_FINE = NC_DEC_FINE, K_COLOR = NC_DEC_COLOR };
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
+
+// Feature index held in register j of lane-group g (C layout).
+__device__ __forceinline__ int feat_of(int j, int g) { return 16 * (j >> 2) + 4 * g + (j & 3); }
+
+// ---------------------------------------------------------------------------
+// Per-decoder layouts.
+//   LDS weight image: every nn.Linear stored row-major [out][packed in] with a
+//   leading dimension padded by 4 floats (16-byte rows, ds_read_b128 A reads,
+//   conflict-free ds_read_b32 transposed reads).  "Packed in" inserts zero
+//   columns so that every input block starts on a 16-feature tile:
+//     L0 (xyz): emb 0..92 | 0 0 0                      -> 96
+//     L3 (xyz): emb 0..92 | 0 0 0 | h2 0..31 (96..127)  -> 128
+//     L3 (coarse, MLP_no_xyz): c 0..31 | h2 32..63      -> 64
+//   Flat parameter vector (gradient output): nn.Module.parameters() order.
+// ---------------------------------------------------------------------------
+template <int KIND>
+struct Net {
+  static constexpr bool XYZ = KIND != K_COARSE;
+  static constexpr int CD = (KIND == K_FINE) ? 64 : 32;   // fc_c input width
+  static constexpr int NOUT = (KIND == K_COLOR) ? 4 : 1;  // output_linear rows
+  static constexpr int NFC = XYZ ? 5 : 0;
+  // real input widths of pts_linears
+  __host__ __device__ static constexpr int in_real(int i) {
+    return i == 0 ? (XYZ ? EMB : HID) : i == 3 ? (XYZ ? (EMB + HID) : (2 * HID)) : HID;
+  }
+  // packed input widths
+  static constexpr int IN0 = XYZ ? EMBP : HID;
+  static constexpr int IN3 = XYZ ? (EMBP + HID) : (2 * HID);
+  static constexpr int LD0 = IN0 + 4, LDH = HID + 4, LD3 = IN3 + 4, LDC = CD + 4;
+  // LDS offsets (floats)
+  static constexpr int W0 = 0;
+  static constexpr int W1 = W0 + HID * LD0;
+  static constexpr int W2 = W1 + HID * LDH;
+  static constexpr int W3 = W2 + HID * LDH;
+  static constexpr int W4 = W3 + HID * LD3;
+  static constexpr int WC = W4 + HID * LDH;      // NFC x [32][LDC]
+  static constexpr int BL = WC + NFC * HID * LDC;  // 5 x 32 linear biases
+  static constexpr int BC = BL + 5 * HID;          // NFC x 32 fc biases
+  static constexpr int WO = BC + NFC * HID;        // [4][32] output weights (rows >= NOUT zero)
+  static constexpr int BO = WO + 4 * HID;          // [4]
+  static constexpr int FB = BO + 4;                // [3][96] Fourier B (XYZ)
+  static constexpr int WEIGHTS = ((FB + (XYZ ? 3 * EMBP : 0)) + 3) & ~3;
+  __host__ __device__ static constexpr int lin_off(int i) {
+    return i == 0 ? W0 : i == 1 ? W1 : i == 2 ? W2 : i == 3 ? W3 : W4;
+  }
+  __host__ __device__ static constexpr int lin_ld(int i) { return i == 0 ? LD0 : i == 3 ? LD3 : LDH; }
+  // packed column of a real input column of pts_linears[i]
+  __host__ __device__ static constexpr int pack_col(int i, int c) {
+    return (XYZ && (i == 0 || i == 3) && c >= EMB) ? (c - EMB + EMBP) : c;
+  }
+  // real column of a packed column (-1: padding)
+  __host__ __device__ static constexpr int real_col(int i, int c) {
+    return (XYZ && (i == 0 || i == 3)) ? (c < EMB ? c : (c < EMBP ? -1 : c - EMBP + EMB)) : c;
+  }
+
+  // flat parameter offsets (reference parameters() order)
+  static constexpr int64_t FC_BLOCK = (int64_t)HID * CD + HID;
+  __host__ __device__ static constexpr int64_t p_fc_w(int i) { return XYZ ? i * FC_BLOCK : 0; }
+  __host__ __device__ static constexpr int64_t p_fc_b(int i) { return p_fc_w(i) + (int64_t)HID * CD; }
+  static constexpr int64_t P_B = XYZ ? 5 * FC_BLOCK : 0;
+  static constexpr int64_t P_LIN0 = XYZ ? P_B + 3 * EMB : 0;
+  __host__ __device__ static constexpr int64_t p_lin_w(int i) {
+    int64_t o = P_LIN0;
+    for (int k = 0; k < i; ++k) o += (int64_t)HID * in_real(k) + HID;
+    return o;
+  }
+  __host__ __device__ static constexpr int64_t p_lin_b(int i) { return p_lin_w(i) + (int64_t)HID * in_real(i); }
+  static constexpr int64_t P_OUT_W = p_lin_b(4) + HID;
+  static constexpr int64_t P_OUT_B = P_OUT_W + NOUT * HID;
+  static constexpr int64_t NPARAM = P_OUT_B + NOUT;
+};
+
+// ---------------------------------------------------------------------------
+// Trilinear corners of F.grid_sample(5-D, bilinear, border, align_corners=True)
+// restated from ATen's CPU grid_sampler_3d (the reference runs it through
+// decoder.py:186): unnormalise ((x+1)/2)*(size-1), clip to [0, size-1], corner
+// weights as products in x, y, z order, corners tnw..bse (bit0 = x, bit1 = y,
+// bit2 = z).  Compiled with -ffp-contract=off, so the forward value is
+// bit-identical to the CPU reference.
+// ---------------------------------------------------------------------------
+struct Corners {
+  int64_t off[8];  // element offset of the corner (channel 0) in the grid
+  float w[8];      // interpolation weight (0 where the corner is out of bounds)
+  float wx[2], wy[2], wz[2];  // per-axis factors [west/east], [north/south], [top/bottom]
+  float gmx, gmy, gmz;        // d(ix)/d(x_norm) incl. border-clip gradient
+  unsigned inb;                // bit k: corner k inside the grid
+  int64_t x0, y0, z0;          // corner 0 (tnw) voxel coordinates
+};
+
+__device__ __forceinline__ float clip_fwd(float v, float hi) {
+  float t = (v < 0.f) ? 0.f : v;       // std::max(in, 0)
+  return (t < hi) ? t : hi;            // std::min(hi, t)
+}
+
+__device__ __forceinline__ void make_corners(const nc_grid& G, const float xyz[3], Corners& c) {
+  const int64_t D = G.dims[0], H = G.dims[1], W = G.dims[2];
+  const float sx = (float)(W - 1), sy = (float)(H - 1), sz = (float)(D - 1);
+  float ix = ((xyz[0] + 1.f) / 2.f) * sx;
+  float iy = ((xyz[1] + 1.f) / 2.f) * sy;
+  float iz = ((xyz[2] + 1.f) / 2.f) * sz;
+  // border clip gradient: borders count as clipped (GridSampler.h clip_coordinates_set_grad)
+  c.gmx = (ix <= 0.f || ix >= sx) ? 0.f : sx / 2.f;
+  c.gmy = (iy <= 0.f || iy >= sy) ? 0.f : sy / 2.f;
+  c.gmz = (iz <= 0.f || iz >= sz) ? 0.f : sz / 2.f;
+  ix = clip_fwd(ix, sx);
+  iy = clip_fwd(iy, sy);
+  iz = clip_fwd(iz, sz);
+  const int64_t x0 = (int64_t)floorf(ix), y0 = (int64_t)floorf(iy), z0 = (int64_t)floorf(iz);
+  c.x0 = x0; c.y0 = y0; c.z0 = z0;
+  const float fx0 = (float)x0, fy0 = (float)y0, fz0 = (float)z0;
+  const float fx1 = (float)(x0 + 1), fy1 = (float)(y0 + 1), fz1 = (float)(z0 + 1);
+  c.wx[0] = fx1 - ix; c.wx[1] = ix - fx0;
+  c.wy[0] = fy1 - iy; c.wy[1] = iy - fy0;
+  c.wz[0] = fz1 - iz; c.wz[1] = iz - fz0;
+  c.inb = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int xb = k & 1, yb = (k >> 1) & 1, zb = k >> 2;
+    const int64_t xx = x0 + xb, yy = y0 + yb, zz = z0 + zb;
+    const bool in = (xx >= 0 && xx < W && yy >= 0 && yy < H && zz >= 0 && zz < D);
+    c.inb |= (in ? 1u : 0u) << k;
+    c.off[k] = in ? (zz * G.stride[1] + yy * G.stride[2] + xx * G.stride[3]) : 0;
+    c.w[k] = (c.wx[xb] * c.wy[yb]) * c.wz[zb];
+  }
+}
+
+// Gather the 8 channels of lane-group g (C layout: channel 16*(j>>2) + 4g + (j&3))
+// and accumulate them corner by corner in the reference order (no FMA).
+template <bool VEC>
+__device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int g, float out[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = 0.f;
+  const int64_t sC = G.stride[0];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (!((c.inb >> k) & 1u)) continue;
+    const float* base = G.data + c.off[k];
+    float v[8];
+    if (VEC) {
+      const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
+      const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = base[(int64_t)feat_of(j, g) * sC];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = out[j] + v[j] * c.w[k];
+  }
+}
+
+__device__ __forceinline__ bool grid_vec_ok(const nc_grid& G) {
+  return G.stride[0] == 1 && ((reinterpret_cast<uintptr_t>(G.data) & 15u) == 0) &&
+         (G.stride[1] % 4 == 0) && (G.stride[2] % 4 == 0) && (G.stride[3] % 4 == 0);
+}
+
+// normalize_3d_coordinate (common.py:280-295) in float64, then .float()
+__device__ __forceinline__ void normalize_pt(const double p[3], const double (&b)[3][2], float out[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = (float)(((p[k] - b[k][0]) / (b[k][1] - b[k][0])) * 2.0 - 1.0);
+}
+
+// Wavefront reductions over the four lanes of a point (lane-groups g).
+__device__ __forceinline__ float sum_groups(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+}  // namespace nc

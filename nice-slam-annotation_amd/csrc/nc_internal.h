@@ -1,0 +1,107 @@
+// nc_internal.h — kernel argument blocks and launch wrappers shared by the
+// ABI layer (nc_abi.hip) and the kernels (nc_rays.hip, nc_mlp.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nicecore.h"
+
+namespace nc {
+
+// One decoder evaluation in a stage (decoder.py:341-370): which decoder, its
+// output slot, and which gradients the backward must produce for it.
+struct Job {
+  int32_t kind;        // enum nc_decoder
+  int32_t slot;        // index into the per-slot point buffers
+  int32_t need_dw;     // decoder parameter gradient
+  int32_t need_grid;   // gradient into its own grid (the fine decoder's middle lookup never has one)
+  int32_t need_coord;  // gradient into the sample points
+  int32_t pad;
+};
+
+constexpr int MAX_JOBS = 3;
+
+// Arguments of the point-batched decoder kernels.
+struct MlpCtx {
+  int64_t P;                 // number of points
+  int32_t n_jobs;
+  int32_t slab_wgs;          // workgroups per job in the backward launch (= gridDim.x)
+  Job jobs[MAX_JOBS];
+  nc_grid grids[4];
+  nc_decoder_params dec[4];
+  const double* pts;         // [P,3] float64 sample points
+  float* occ;                // [n_jobs][P] occupancy outputs (occupancy decoders)
+  float* rgb;                // [P][3] colour-decoder outputs (channels 0..2)
+  const float* gocc;         // [P] d loss / d occupancy (shared by the occupancy decoders)
+  const float* grgb;         // [P][3] d loss / d rgb
+  double* dpts;              // [n_jobs][P][3] per-decoder point gradients
+  float* slab;               // [n_jobs][slab_wgs][slab_stride] per-workgroup parameter gradients
+  int64_t slab_stride;
+};
+
+// Arguments of the per-ray kernels (sampling, compositing, ray gradients).
+struct RayCtx {
+  int64_t N;
+  int64_t P;
+  int32_t S;             // samples per ray
+  int32_t n_strat, n_surf;
+  int32_t stage;
+  int32_t occ_a, occ_b;  // occupancy slots summed into raw[...,3] (-1: none)
+  int32_t has_rgb;
+  int32_t n_jobs;
+  const float* rays_o;
+  const float* rays_d;
+  const float* gt_depth;
+  const float* depth_max;  // device scalar (user override or computed into the workspace)
+  double bound[3][2];
+  float t_strat[NC_MAX_SAMPLES];
+  double t_surf[NC_MAX_SURF];
+  double* z;             // [N][S]
+  double* pts;           // [P][3]
+  const float* occ;      // [n_jobs][P]
+  const float* rgb;      // [P][3]
+  double* depth;
+  double* var;
+  float* color;
+  const double* g_depth;
+  const double* g_var;
+  const float* g_color;
+  float* gocc;           // [P]
+  float* grgb;           // [P][3]
+  const double* dpts;    // [n_jobs][P][3]
+  float* g_rays_o;
+  float* g_rays_d;
+};
+
+struct ParamReduceCtx {
+  int32_t n_jobs;
+  int32_t slab_wgs;
+  int64_t slab_stride;
+  Job jobs[MAX_JOBS];
+  float* grad[MAX_JOBS];
+  int64_t nparam[MAX_JOBS];
+  const float* slab;
+};
+
+// kernels: launch wrappers (return hipError_t as int)
+int launch_depth_max(const float* gt, int64_t n, float* out, hipStream_t s);
+int launch_ray_setup(const RayCtx& c, hipStream_t s);
+int launch_composite_fwd(const RayCtx& c, hipStream_t s);
+int launch_composite_bwd(const RayCtx& c, hipStream_t s);
+int launch_ray_grads(const RayCtx& c, hipStream_t s);
+int launch_param_reduce(const ParamReduceCtx& c, int64_t max_nparam, hipStream_t s);
+int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s);
+int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, float* gocc, float* grgb,
+                             hipStream_t s);
+int launch_points_grads(const MlpCtx& m, double* g_pts, hipStream_t s);
+
+int mlp_fwd_lds_bytes();
+int mlp_bwd_lds_bytes();
+int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);
+int launch_mlp_bwd(const MlpCtx& c, hipStream_t s);
+int64_t max_param_count();
+
+constexpr int FWD_THREADS = 512;  // 8 waves, 128 points per workgroup iteration
+constexpr int BWD_THREADS = 256;  // 4 waves, 64 points per workgroup sub-chunk
+
+}  // namespace nc

@@ -1,0 +1,367 @@
+// nc_rays.hip — per-ray stages of Renderer.render_batch_ray on gfx950.
+//
+// One wavefront per ray, lane = sample (S = N_samples + N_surface <= 64):
+//   k_ray_setup      Renderer.py:120-231  near/far, bbox slab test, stratified +
+//                    surface samples, 64-lane bitonic merge-sort, float64 points
+//   k_composite_fwd  common.py:215-256 (occupancy=True) + Renderer.py:87 mask:
+//                    alpha, exclusive transmittance product by a wavefront scan,
+//                    depth / variance (float64) and colour
+//   k_composite_bwd  its autograd backward: d occupancy and d rgb per sample,
+//                    the transmittance term by a reverse affine wavefront scan
+//   k_ray_grads      d rays_o / d rays_d from the per-decoder point gradients
+//   k_param_reduce   sum of the per-workgroup weight-gradient slabs
+// All floating-point expressions keep the reference's association order and the
+// file is compiled with -ffp-contract=off, so the sample depths and points are
+// bit-identical to the CPU reference.
+#include <math.h>
+
+#include "nc_device.h"
+#include "nc_internal.h"
+
+namespace nc {
+
+constexpr int RAY_WAVES = 4;  // rays per 256-thread workgroup
+
+__global__ void __launch_bounds__(1024) k_depth_max(const float* gt, int64_t n, float* out) {
+  __shared__ float red[16];
+  float m = -INFINITY;
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const float v = gt[k];
+    m = (v > m || isnan(v)) ? v : m;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v = __shfl_xor(m, o);
+    m = (v > m || isnan(v)) ? v : m;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = (red[w] > r || isnan(red[w])) ? red[w] : r;
+    *out = r;
+  }
+}
+
+__device__ __forceinline__ bool gt_nan_last(double a, double b) {  // a > b, NaN largest (torch.sort)
+  return (isnan(a) && !isnan(b)) || a > b;
+}
+
+__device__ __forceinline__ double max_nan(double a, double b) { return (a > b || isnan(a)) ? a : b; }
+__device__ __forceinline__ double min_nan(double a, double b) { return (a < b || isnan(a)) ? a : b; }
+
+__global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  if (r >= c.N) return;
+  double o[3], d[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    o[k] = (double)c.rays_o[r * 3 + k];
+    d[k] = (double)c.rays_d[r * 3 + k];
+  }
+  // Renderer.py:139-152: far_bb = min_axis(max(t0, t1)) + 0.01 (no grad, float64)
+  double far_bb = 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double t0 = (c.bound[k][0] - o[k]) / d[k];
+    const double t1 = (c.bound[k][1] - o[k]) / d[k];
+    const double mk = max_nan(t0, t1);
+    far_bb = (k == 0) ? mk : min_nan(far_bb, mk);
+  }
+  far_bb = far_bb + 0.01;
+  const bool has_depth = c.n_surf > 0 || c.gt_depth != nullptr;
+  double far = far_bb;
+  float gd = 0.f, dmax = 0.f;
+  if (has_depth) {
+    gd = c.gt_depth[r];
+    dmax = *c.depth_max;
+    const double hi = (double)(dmax * 1.2f);  // torch.max(gt_depth*1.2) (float32)
+    double v = far_bb < 0.0 ? 0.0 : far_bb;   // torch.clamp(far_bb, 0, hi)
+    far = v > hi ? hi : v;
+  }
+  double z;
+  if (lane < c.n_strat) {
+    const float t = c.t_strat[lane];
+    const float om = 1.0f - t;                               // (1.-t_vals)
+    const float nearw = has_depth ? (gd * 0.01f) * om : 0.01f * om;  // near*(1-t), float32
+    z = (double)nearw + far * (double)t;                     // + far*t (float64)
+  } else if (lane < c.n_strat + c.n_surf) {
+    const double ts = c.t_surf[lane - c.n_strat];
+    if (gd > 0.f) {  // Renderer.py:185-187
+      z = (double)(0.95f * gd) * (1.0 - ts) + (double)(1.05f * gd) * ts;
+    } else {         // Renderer.py:193-196
+      z = 0.001 * (1.0 - ts) + (double)dmax * ts;
+    }
+  } else {
+    z = INFINITY;
+  }
+  if (c.n_surf > 0) {  // Renderer.py:222-224 torch.sort of the 48 depths (bitonic, 64 lanes)
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const double other = __shfl_xor(z, j);
+        const bool up = (lane & k) == 0;
+        const bool lower = (lane & j) == 0;
+        const bool take_min = (lower == up);
+        const bool zg = gt_nan_last(z, other);
+        z = take_min ? (zg ? other : z) : (zg ? z : other);
+      }
+    }
+  }
+  if (lane < c.S) {
+    const int64_t p = r * c.S + lane;
+    c.z[p] = z;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c.pts[p * 3 + k] = o[k] + d[k] * z;  // Renderer.py:227-228
+  }
+}
+
+// strict in-bound mask of Renderer.py:63-66 against the renderer bound
+__device__ __forceinline__ bool in_bound(const double* p, const double (&b)[3][2]) {
+  return p[0] < b[0][1] && p[0] > b[0][0] && p[1] < b[1][1] && p[1] > b[1][0] && p[2] < b[2][1] &&
+         p[2] > b[2][0];
+}
+
+struct SampleState {
+  double z;
+  float a, q, T, w;
+  float rgb[3];
+  bool inb;
+};
+
+// shared by forward and backward: alpha, exclusive product T, weights
+__device__ __forceinline__ void sample_state(const RayCtx& c, int64_t r, int lane, SampleState& s) {
+  const bool act = lane < c.S;
+  const int64_t p = r * c.S + (act ? lane : 0);
+  s.z = act ? c.z[p] : 0.0;
+  float occ = 0.f;
+  if (c.occ_a >= 0) occ = c.occ[(int64_t)c.occ_a * c.P + p];
+  if (c.occ_b >= 0) occ = occ + c.occ[(int64_t)c.occ_b * c.P + p];  // fine_occ + middle_occ
+  s.inb = in_bound(c.pts + p * 3, c.bound);
+  if (!s.inb) occ = 100.f;  // Renderer.py:87
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.rgb[k] = c.has_rgb ? c.rgb[p * 3 + k] : 0.f;
+  const float x = 10.f * occ;
+  s.a = 1.f / (1.f + expf(-x));          // torch.sigmoid
+  s.q = act ? (1.f - s.a) + 1e-10f : 1.f; // (1.-alpha + 1e-10)
+  // exclusive prefix product over the wavefront (Hillis-Steele on 64 lanes)
+  float incl = s.q;
+#pragma unroll
+  for (int dlt = 1; dlt < 64; dlt <<= 1) {
+    const float v = __shfl_up(incl, dlt);
+    if (lane >= dlt) incl = incl * v;
+  }
+  const float ex = __shfl_up(incl, 1);
+  s.T = lane == 0 ? 1.f : ex;
+  s.w = act ? s.a * s.T : 0.f;
+  if (!act) {
+    s.a = 0.f;
+    s.rgb[0] = s.rgb[1] = s.rgb[2] = 0.f;
+  }
+}
+
+__device__ __forceinline__ double wsum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wsum_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) k_composite_fwd(const RayCtx c) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  if (r >= c.N) return;
+  SampleState s;
+  sample_state(c, r, lane, s);
+  const float cr = wsum_f(s.w * s.rgb[0]);
+  const float cg = wsum_f(s.w * s.rgb[1]);
+  const float cb = wsum_f(s.w * s.rgb[2]);
+  const double depth = wsum_d((double)s.w * s.z);
+  const double tmp = s.z - depth;
+  const double var = wsum_d(lane < c.S ? ((double)s.w * tmp) * tmp : 0.0);
+  if (lane == 0) {
+    c.depth[r] = depth;
+    c.var[r] = var;
+    c.color[r * 3 + 0] = cr;
+    c.color[r * 3 + 1] = cg;
+    c.color[r * 3 + 2] = cb;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  if (r >= c.N) return;
+  const bool act = lane < c.S;
+  SampleState s;
+  sample_state(c, r, lane, s);
+  const double depth = wsum_d((double)s.w * s.z);
+  const double gD = c.g_depth ? c.g_depth[r] : 0.0;
+  const double gV = c.g_var ? c.g_var[r] : 0.0;
+  float gC[3] = {0.f, 0.f, 0.f};
+  if (c.g_color) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gC[k] = c.g_color[r * 3 + k];
+  }
+  // var = sum w (z-D)^2, D = sum w z  (common.py:253-255)
+  const double tmp = s.z - depth;
+  const double gtmp = act ? 2.0 * gV * (double)s.w * tmp : 0.0;
+  const double gDt = gD - wsum_d(gtmp);
+  float gw = (float)(gDt * s.z) + (float)(gV * tmp * tmp);
+  gw = gw + (gC[0] * s.rgb[0] + gC[1] * s.rgb[1] + gC[2] * s.rgb[2]);
+  if (!act) gw = 0.f;
+  // w = a * T, T_i = prod_{j<i} q_j, q = 1 - a + 1e-10
+  const float gT = gw * s.a;
+  // S_l = sum_{i>l} gT_i prod_{l<k<i} q_k  -> reverse scan of x -> b_l + c_l x
+  float cB = __shfl_down(gT, 1);
+  float cC = __shfl_down(s.q, 1);
+  if (lane + 1 >= c.S) { cB = 0.f; cC = 0.f; }
+#pragma unroll
+  for (int dlt = 1; dlt < 64; dlt <<= 1) {
+    const float nb = __shfl_down(cB, dlt);
+    const float ncc = __shfl_down(cC, dlt);
+    if (lane + dlt < 64) {
+      cB = cB + cC * nb;
+      cC = cC * ncc;
+    }
+  }
+  const float gq = s.T * cB;
+  const float ga = gw * s.T - gq;
+  const float gy = (ga * (1.f - s.a)) * s.a;  // sigmoid backward
+  float g_occ = gy * 10.f;
+  if (!s.inb) g_occ = 0.f;
+  if (act) {
+    const int64_t p = r * c.S + lane;
+    c.gocc[p] = g_occ;
+    if (c.has_rgb) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) c.grgb[p * 3 + k] = gC[k] * s.w;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_ray_grads(const RayCtx c) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  if (r >= c.N) return;
+  const bool act = lane < c.S;
+  const int64_t p = r * c.S + (act ? lane : 0);
+  double dp[3] = {0.0, 0.0, 0.0};
+  if (act) {
+    for (int j = 0; j < c.n_jobs; ++j) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dp[k] += c.dpts[((int64_t)j * c.P + p) * 3 + k];
+    }
+  }
+  const double z = act ? c.z[p] : 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double go = wsum_d(dp[k]);
+    const double gd = wsum_d(dp[k] * z);
+    if (lane == 0) {
+      if (c.g_rays_o) c.g_rays_o[r * 3 + k] = (float)go;
+      if (c.g_rays_d) c.g_rays_d[r * 3 + k] = (float)gd;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_param_reduce(const ParamReduceCtx c) {
+  const int j = blockIdx.y;
+  // constant-index selects (dynamic indexing of the argument block spills it)
+  const Job job = j == 0 ? c.jobs[0] : (j == 1 ? c.jobs[1] : c.jobs[2]);
+  float* grad = j == 0 ? c.grad[0] : (j == 1 ? c.grad[1] : c.grad[2]);
+  const int64_t np = j == 0 ? c.nparam[0] : (j == 1 ? c.nparam[1] : c.nparam[2]);
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!job.need_dw || grad == nullptr || e >= np) return;
+  const float* src = c.slab + (int64_t)j * c.slab_wgs * c.slab_stride + e;
+  float s = 0.f;
+  for (int w = 0; w < c.slab_wgs; ++w) s += src[(int64_t)w * c.slab_stride];
+  grad[e] = s;
+}
+
+// ---- NICE.forward on caller points (decoder.py:336-370) ----
+__global__ void k_points_assemble(const MlpCtx m, int stage, float* raw) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m.P) return;
+  float o[4] = {0.f, 0.f, 0.f, 0.f};
+  if (stage == NC_STAGE_COLOR) {
+    o[0] = m.rgb[p * 3 + 0];
+    o[1] = m.rgb[p * 3 + 1];
+    o[2] = m.rgb[p * 3 + 2];
+  }
+  if (stage == NC_STAGE_FINE || stage == NC_STAGE_COLOR) o[3] = m.occ[p] + m.occ[m.P + p];  // fine + middle
+  else o[3] = m.occ[p];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) raw[p * 4 + k] = o[k];
+}
+
+__global__ void k_points_split_grad(const MlpCtx m, int stage, const float* g_raw, float* gocc, float* grgb) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m.P) return;
+  gocc[p] = g_raw[p * 4 + 3];
+  if (stage == NC_STAGE_COLOR) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) grgb[p * 3 + k] = g_raw[p * 4 + k];
+  }
+}
+
+__global__ void k_points_grads(const MlpCtx m, double* g_pts) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m.P) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double s = 0.0;
+    for (int j = 0; j < m.n_jobs; ++j) s += m.dpts[((int64_t)j * m.P + p) * 3 + k];
+    g_pts[p * 3 + k] = s;
+  }
+}
+
+// ---- launch wrappers ----
+static inline unsigned ray_blocks(int64_t n) { return (unsigned)((n + RAY_WAVES - 1) / RAY_WAVES); }
+
+int launch_depth_max(const float* gt, int64_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_depth_max, dim3(1), dim3(1024), 0, s, gt, n, out);
+  return (int)hipGetLastError();
+}
+int launch_ray_setup(const RayCtx& c, hipStream_t s) {
+  hipLaunchKernelGGL(k_ray_setup, dim3(ray_blocks(c.N)), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_composite_fwd(const RayCtx& c, hipStream_t s) {
+  hipLaunchKernelGGL(k_composite_fwd, dim3(ray_blocks(c.N)), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_composite_bwd(const RayCtx& c, hipStream_t s) {
+  hipLaunchKernelGGL(k_composite_bwd, dim3(ray_blocks(c.N)), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_ray_grads(const RayCtx& c, hipStream_t s) {
+  hipLaunchKernelGGL(k_ray_grads, dim3(ray_blocks(c.N)), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_param_reduce(const ParamReduceCtx& c, int64_t max_nparam, hipStream_t s) {
+  dim3 grid((unsigned)((max_nparam + 255) / 256), c.n_jobs);
+  hipLaunchKernelGGL(k_param_reduce, grid, dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s) {
+  hipLaunchKernelGGL(k_points_assemble, dim3((unsigned)((m.P + 255) / 256)), dim3(256), 0, s, m, stage, raw);
+  return (int)hipGetLastError();
+}
+int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, float* gocc, float* grgb,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_points_split_grad, dim3((unsigned)((m.P + 255) / 256)), dim3(256), 0, s, m, stage,
+                     g_raw, gocc, grgb);
+  return (int)hipGetLastError();
+}
+int launch_points_grads(const MlpCtx& m, double* g_pts, hipStream_t s) {
+  hipLaunchKernelGGL(k_points_grads, dim3((unsigned)((m.P + 255) / 256)), dim3(256), 0, s, m, g_pts);
+  return (int)hipGetLastError();
+}
+
+}  // namespace nc

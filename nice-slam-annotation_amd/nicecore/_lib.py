@@ -1,0 +1,137 @@
+"""ctypes binding of libnicecore.so (include/nicecore.h).
+
+The product path calls ONLY this library for the render hot path; if it cannot
+be loaded on a HIP device the call fails loudly (no PyTorch fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnicecore.so")
+
+NC_ABI_VERSION = 1
+NC_MAX_SAMPLES = 64
+NC_MAX_SURF = 32
+
+STAGES = {"coarse": 0, "middle": 1, "fine": 2, "color": 3}
+DEC_COARSE, DEC_MIDDLE, DEC_FINE, DEC_COLOR = 0, 1, 2, 3
+DECODER_NAMES = ("coarse", "middle", "fine", "color")
+GRID_KEYS = ("grid_coarse", "grid_middle", "grid_fine", "grid_color")
+# decoders (enum nc_decoder) evaluated per stage (decoder.py:341-370)
+STAGE_DECODERS = {0: (DEC_COARSE,), 1: (DEC_MIDDLE,), 2: (DEC_FINE, DEC_MIDDLE),
+                  3: (DEC_FINE, DEC_MIDDLE, DEC_COLOR)}
+# grids each stage reads (the fine decoder also samples grid_middle, decoder.py:199-201)
+STAGE_GRIDS = {0: (0,), 1: (1,), 2: (1, 2), 3: (1, 2, 3)}
+
+
+class NcGrid(ctypes.Structure):
+    _fields_ = [("data", c_void_p), ("grad", c_void_p), ("dims", c_int64 * 3),
+                ("stride", c_int64 * 4), ("grad_stride", c_int64 * 4)]
+
+
+class NcDecoderParams(ctypes.Structure):
+    _fields_ = [("fc_w", c_void_p * 5), ("fc_b", c_void_p * 5), ("fourier_B", c_void_p),
+                ("lin_w", c_void_p * 5), ("lin_b", c_void_p * 5), ("out_w", c_void_p),
+                ("out_b", c_void_p), ("grad", c_void_p), ("bound", (c_double * 2) * 3)]
+
+
+class NcRenderArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("stage", c_int32), ("n_rays", c_int64),
+                ("n_strat", c_int32), ("n_surf", c_int32),
+                ("rays_o", c_void_p), ("rays_d", c_void_p), ("gt_depth", c_void_p),
+                ("depth_max", c_void_p), ("bound", (c_double * 2) * 3),
+                ("t_strat", c_float * NC_MAX_SAMPLES), ("t_surf", c_double * NC_MAX_SURF),
+                ("grids", NcGrid * 4), ("dec", NcDecoderParams * 4),
+                ("depth", c_void_p), ("var", c_void_p), ("color", c_void_p),
+                ("g_depth", c_void_p), ("g_var", c_void_p), ("g_color", c_void_p),
+                ("g_rays_o", c_void_p), ("g_rays_d", c_void_p)]
+
+
+class NcPointsArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("stage", c_int32), ("n_points", c_int64),
+                ("pts", c_void_p), ("grids", NcGrid * 4), ("dec", NcDecoderParams * 4),
+                ("raw", c_void_p), ("g_raw", c_void_p), ("g_pts", c_void_p)]
+
+
+EXPORTS = {
+    "nc_abi_version": (c_int, []),
+    "nc_last_error": (ctypes.c_char_p, []),
+    "nc_param_count": (c_int64, [c_int]),
+    "nc_struct_size": (c_size_t, [c_int]),
+    "nc_render_workspace_bytes": (c_size_t, [POINTER(NcRenderArgs)]),
+    "nc_render_forward": (c_int, [POINTER(NcRenderArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_render_backward": (c_int, [POINTER(NcRenderArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_timing_start": (c_int, [ctypes.c_uint32]),
+    "nc_timing_stop": (c_int, [POINTER(c_double), POINTER(c_int64), c_int]),
+    "nc_kernel_name": (ctypes.c_char_p, [c_int]),
+    "nc_points_workspace_bytes": (c_size_t, [POINTER(NcPointsArgs)]),
+    "nc_points_forward": (c_int, [POINTER(NcPointsArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_points_backward": (c_int, [POINTER(NcPointsArgs), c_void_p, c_size_t, c_void_p]),
+}
+
+_lib = None
+
+
+class NiceCoreError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and type the exports of libnicecore.so."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or os.environ.get("NICECORE_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise NiceCoreError(
+            f"libnicecore.so not found at {p}; build it with `python -m nicecore.build` "
+            "(hipcc --offload-arch=gfx950). There is no CPU/PyTorch fallback.")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.nc_abi_version() != NC_ABI_VERSION:
+        raise NiceCoreError("libnicecore.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().nc_last_error()
+        raise NiceCoreError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_fwd": 3,
+              "k_composite_bwd": 4, "k_mlp_bwd": 5, "k_param_reduce": 6, "k_ray_grads": 7,
+              "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10}
+
+
+class KernelTimer:
+    """HIP-event timing of the library's kernels on their launch stream."""
+
+    def __init__(self, kernels=None):
+        ids = KERNEL_IDS.values() if kernels is None else [KERNEL_IDS[k] for k in kernels]
+        self.mask = 0
+        for i in ids:
+            self.mask |= 1 << i
+        self.result = {}
+
+    def __enter__(self):
+        load().nc_timing_start(self.mask)
+        return self
+
+    def __exit__(self, *exc):
+        lib = load()
+        n = 16
+        ms = (c_double * n)()
+        cnt = (c_int64 * n)()
+        k = lib.nc_timing_stop(ms, cnt, n)
+        if k < 0:
+            check(k, "nc_timing_stop")
+        self.result = {lib.nc_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(k) if cnt[i] > 0}
+        return False

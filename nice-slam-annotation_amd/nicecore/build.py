@@ -1,0 +1,64 @@
+"""Build libnicecore.so (HIP, gfx950) in-tree with hipcc.
+
+    python -m nicecore.build            # from nice-slam-annotation_amd/
+    python nice-slam-annotation_amd/nicecore/build.py
+
+The library is plain C ABI (include/nicecore.h); it does not link against torch.
+-ffp-contract=off keeps the reference's float association (ray sampling and
+trilinear weights are bit-identical to the CPU path); FMAs the kernels want are
+explicit (__builtin_fmaf, MFMA).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+REPO = os.path.dirname(PKG_ROOT)
+CSRC = os.path.join(PKG_ROOT, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+LIB = os.path.join(HERE, "libnicecore.so")
+SOURCES = ["nc_abi.hip", "nc_rays.hip", "nc_mlp.hip"]
+ARCH = os.environ.get("NICECORE_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libnicecore.so)")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "nicecore.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False, extra=()) -> str:
+    if not force and not needs_build():
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+           "-I", INCLUDE, "-I", CSRC, *extra, "-o", LIB + ".tmp",
+           *[os.path.join(CSRC, s) for s in SOURCES]]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+    if verbose and (r.stdout or r.stderr):
+        print(r.stdout + r.stderr)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    extra = ["-Rpass-analysis=kernel-resource-usage"] if "--resources" in sys.argv else []
+    print(build(force=force or bool(extra), verbose=True, extra=extra))

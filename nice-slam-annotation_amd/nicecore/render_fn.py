@@ -1,0 +1,329 @@
+"""torch.autograd.Function wrappers around libnicecore.so.
+
+``NiceRenderFn``   = Renderer.render_batch_ray (src/utils/Renderer.py:95-262) forward +
+                     autograd backward, in two C-ABI calls.
+``NiceEvalFn``     = NICE.forward (src/conv_onet/models/decoder.py:336-370) on caller
+                     points.
+
+Tensors are handed over as raw device pointers + strides; the library enqueues on
+the current HIP stream and never synchronises.  Gradients honour
+``ctx.needs_input_grad``: grids / decoder parameters / rays that do not need a
+gradient are not computed (the tracker's ray-only mode skips every weight
+gradient and grid scatter).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _bound_rows(b) -> list:
+    b = torch.as_tensor(b).detach().to("cpu", torch.float64).reshape(3, 2)
+    return [[float(b[k, 0]), float(b[k, 1])] for k in range(3)]
+
+
+def decoder_modules(decoders):
+    return [getattr(decoders, n + "_decoder", None) for n in L.DECODER_NAMES]
+
+
+def decoder_params(module, kind: int) -> list:
+    """Parameters of one decoder in nn.Module.parameters() order (the flat-gradient
+    order of the ABI)."""
+    ps = []
+    if kind != L.DEC_COARSE:
+        for i in range(5):
+            ps += [module.fc_c[i].weight, module.fc_c[i].bias]
+        ps.append(module.embedder._B)
+    for i in range(5):
+        ps += [module.pts_linears[i].weight, module.pts_linears[i].bias]
+    ps += [module.output_linear.weight, module.output_linear.bias]
+    return ps
+
+
+def _check_param(t, device):
+    if t.device != device or t.dtype != torch.float32 or not t.is_contiguous():
+        raise L.NiceCoreError(f"decoder parameters must be contiguous float32 on {device}")
+
+
+def _fill_decoder(nd: L.NcDecoderParams, kind: int, params: list, bound, device):
+    for t in params:
+        _check_param(t, device)
+    k = 0
+    if kind != L.DEC_COARSE:
+        for i in range(5):
+            nd.fc_w[i] = params[k].data_ptr(); nd.fc_b[i] = params[k + 1].data_ptr(); k += 2
+        nd.fourier_B = params[k].data_ptr(); k += 1
+    for i in range(5):
+        nd.lin_w[i] = params[k].data_ptr(); nd.lin_b[i] = params[k + 1].data_ptr(); k += 2
+    nd.out_w = params[k].data_ptr(); nd.out_b = params[k + 1].data_ptr()
+    nd.grad = None
+    rows = _bound_rows(bound)
+    for a in range(3):
+        nd.bound[a][0], nd.bound[a][1] = rows[a]
+
+
+def _fill_grid(ng: L.NcGrid, t, device):
+    if t.dim() != 5 or t.shape[0] != 1 or t.shape[1] != 32:
+        raise L.NiceCoreError(f"feature grid must be [1,32,D,H,W], got {tuple(t.shape)}")
+    if t.dtype != torch.float32 or t.device != device:
+        raise L.NiceCoreError(f"feature grid must be float32 on {device}")
+    ng.data = t.data_ptr()
+    ng.grad = None
+    for a in range(3):
+        ng.dims[a] = t.shape[2 + a]
+    st = t.stride()
+    for a in range(4):
+        ng.stride[a] = st[1 + a]
+        ng.grad_stride[a] = st[1 + a]
+
+
+def _decoder_bound(module, name):
+    b = getattr(module, "bound", None)
+    if b is None:
+        raise L.NiceCoreError(
+            f"{name}_decoder.bound is not set (NICE_SLAM.load_bound assigns it, "
+            "src/NICE_SLAM.py:202-208)")
+    return b
+
+
+class _Plan:
+    """Which decoders / grids a stage touches and how the flat param list splits."""
+
+    def __init__(self, stage: int, decoders):
+        self.stage = stage
+        self.decs = sorted(L.STAGE_DECODERS[stage])
+        self.grids = L.STAGE_GRIDS[stage]
+        mods = decoder_modules(decoders)
+        self.modules = {k: mods[k] for k in self.decs}
+        for k in self.decs:
+            if self.modules[k] is None:
+                raise L.NiceCoreError(f"stage needs the {L.DECODER_NAMES[k]} decoder")
+        self.params = {k: decoder_params(self.modules[k], k) for k in self.decs}
+        self.bounds = {k: _decoder_bound(self.modules[k], L.DECODER_NAMES[k]) for k in self.decs}
+
+    def flat_params(self):
+        out = []
+        for k in self.decs:
+            out += self.params[k]
+        return out
+
+    def param_slices(self):
+        s, o = {}, 0
+        for k in self.decs:
+            n = len(self.params[k])
+            s[k] = (o, o + n)
+            o += n
+        return s
+
+
+def _alloc_param_grads(lib, plan, needs_params, args, device):
+    """flat gradient buffers (one per decoder whose params need grad)."""
+    flats = {}
+    sl = plan.param_slices()
+    for k in plan.decs:
+        a, b = sl[k]
+        if any(needs_params[a:b]):
+            flats[k] = torch.empty(lib.nc_param_count(k), device=device, dtype=torch.float32)
+            args.dec[k].grad = flats[k].data_ptr()
+        else:
+            args.dec[k].grad = None
+    return flats
+
+
+def _split_param_grads(plan, flats, needs_params):
+    out = []
+    sl = plan.param_slices()
+    for k in plan.decs:
+        a, b = sl[k]
+        ps = plan.params[k]
+        if k not in flats:
+            out += [None] * len(ps)
+            continue
+        o = 0
+        for j, p in enumerate(ps):
+            n = p.numel()
+            out.append(flats[k][o:o + n].view_as(p) if needs_params[a + j] else None)
+            o += n
+    return out
+
+
+class NiceRenderFn(torch.autograd.Function):
+    """render_batch_ray on the HIP core.  Inputs: (spec, rays_o, rays_d, gt_depth|None,
+    grid_coarse|None, grid_middle|None, grid_fine|None, grid_color|None, *params)."""
+
+    @staticmethod
+    def forward(ctx, spec, rays_o, rays_d, gt_depth, g0, g1, g2, g3, *params):
+        lib = L.load()
+        plan = spec["plan"]
+        device = rays_o.device
+        if device.type != "cuda":
+            raise L.NiceCoreError("nicecore renders on a HIP device; tensors are on " + str(device))
+        rays_o = rays_o.detach().float().contiguous()
+        rays_d = rays_d.detach().float().contiguous()
+        N = rays_o.shape[0]
+        a = L.NcRenderArgs()
+        a.abi_version = L.NC_ABI_VERSION
+        a.stage = plan.stage
+        a.n_rays = N
+        a.n_strat = spec["n_strat"]
+        a.n_surf = spec["n_surf"]
+        a.rays_o = rays_o.data_ptr()
+        a.rays_d = rays_d.data_ptr()
+        gt = None
+        if gt_depth is not None:
+            gt = gt_depth.detach().reshape(-1).float().contiguous()
+            a.gt_depth = gt.data_ptr()
+        dmax = spec.get("depth_max")
+        if dmax is not None:
+            dmax = dmax.detach().reshape(1).float().contiguous()
+            a.depth_max = dmax.data_ptr()
+        rows = _bound_rows(spec["bound"])
+        for k in range(3):
+            a.bound[k][0], a.bound[k][1] = rows[k]
+        ts, tsurf = spec["t_strat"], spec["t_surf"]
+        for k in range(len(ts)):
+            a.t_strat[k] = float(ts[k])
+        for k in range(len(tsurf)):
+            a.t_surf[k] = float(tsurf[k])
+        grids = (g0, g1, g2, g3)
+        gkeep = []
+        for k in plan.grids:
+            if grids[k] is None:
+                raise L.NiceCoreError(f"stage needs {L.GRID_KEYS[k]}")
+            g = grids[k].detach()
+            _fill_grid(a.grids[k], g, device)
+            gkeep.append(g)
+        for k in plan.decs:
+            _fill_decoder(a.dec[k], k, plan.params[k], plan.bounds[k], device)
+        depth = torch.empty(N, device=device, dtype=torch.float64)
+        var = torch.empty(N, device=device, dtype=torch.float64)
+        color = torch.empty(N, 3, device=device, dtype=torch.float32)
+        a.depth, a.var, a.color = depth.data_ptr(), var.data_ptr(), color.data_ptr()
+        nbytes = lib.nc_render_workspace_bytes(ctypes.byref(a))
+        if nbytes == 0:
+            L.check(-1, "nc_render_workspace_bytes")
+        ws = torch.empty(nbytes, device=device, dtype=torch.uint8)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        L.check(lib.nc_render_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_render_forward")
+        ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
+        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params)
+        ctx.grids = grids
+        return depth, var, color
+
+    @staticmethod
+    def backward(ctx, g_depth, g_var, g_color):
+        lib = L.load()
+        a, plan = ctx.args, ctx.plan
+        need = ctx.needs_input_grad
+        rays_o = ctx.keep[0]
+        device = rays_o.device
+        gd = g_depth.detach().double().contiguous() if g_depth is not None else None
+        gv = g_var.detach().double().contiguous() if g_var is not None else None
+        gc = g_color.detach().float().contiguous() if g_color is not None else None
+        a.g_depth, a.g_var, a.g_color = _ptr(gd), _ptr(gv), _ptr(gc)
+        g_ro = torch.empty_like(rays_o) if need[1] else None
+        g_rd = torch.empty_like(rays_o) if need[2] else None
+        # the kernel computes d rays_o and d rays_d together; ask for both if either is needed
+        if (g_ro is None) != (g_rd is None):
+            g_ro = g_ro if g_ro is not None else torch.empty_like(rays_o)
+            g_rd = g_rd if g_rd is not None else torch.empty_like(rays_o)
+        a.g_rays_o, a.g_rays_d = _ptr(g_ro), _ptr(g_rd)
+        grid_grads = [None] * 4
+        for k in plan.grids:
+            a.grids[k].grad = None
+            if need[4 + k]:
+                gg = torch.zeros_like(ctx.grids[k])  # keeps the grid's memory format
+                st = gg.stride()
+                a.grids[k].grad = gg.data_ptr()
+                for ax in range(4):
+                    a.grids[k].grad_stride[ax] = st[1 + ax]
+                grid_grads[k] = gg
+        needs_params = need[8:]
+        flats = _alloc_param_grads(lib, plan, needs_params, a, device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        L.check(lib.nc_render_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
+                "nc_render_backward")
+        pg = _split_param_grads(plan, flats, needs_params)
+        return (None, g_ro if need[1] else None, g_rd if need[2] else None, None, *grid_grads, *pg)
+
+
+class NiceEvalFn(torch.autograd.Function):
+    """NICE.forward(p, c_grid, stage) on the HIP core.  Inputs: (spec, p, g0..g3, *params)."""
+
+    @staticmethod
+    def forward(ctx, spec, p, g0, g1, g2, g3, *params):
+        lib = L.load()
+        plan = spec["plan"]
+        device = p.device
+        if device.type != "cuda":
+            raise L.NiceCoreError("nicecore evaluates on a HIP device; points are on " + str(device))
+        pts = p.detach().reshape(-1, 3).double().contiguous()
+        P = pts.shape[0]
+        a = L.NcPointsArgs()
+        a.abi_version = L.NC_ABI_VERSION
+        a.stage = plan.stage
+        a.n_points = P
+        a.pts = pts.data_ptr()
+        grids = (g0, g1, g2, g3)
+        gkeep = []
+        for k in plan.grids:
+            if grids[k] is None:
+                raise L.NiceCoreError(f"stage needs {L.GRID_KEYS[k]}")
+            g = grids[k].detach()
+            _fill_grid(a.grids[k], g, device)
+            gkeep.append(g)
+        for k in plan.decs:
+            _fill_decoder(a.dec[k], k, plan.params[k], plan.bounds[k], device)
+        raw = torch.empty(P, 4, device=device, dtype=torch.float32)
+        a.raw = raw.data_ptr()
+        nbytes = lib.nc_points_workspace_bytes(ctypes.byref(a))
+        ws = torch.empty(max(nbytes, 1), device=device, dtype=torch.uint8)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        L.check(lib.nc_points_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_points_forward")
+        ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
+        ctx.keep = (pts, gkeep, params)
+        ctx.grids = grids
+        ctx.p_dtype, ctx.p_shape = p.dtype, p.shape
+        return raw
+
+    @staticmethod
+    def backward(ctx, g_raw):
+        lib = L.load()
+        a, plan = ctx.args, ctx.plan
+        need = ctx.needs_input_grad
+        pts = ctx.keep[0]
+        device = pts.device
+        gr = g_raw.detach().float().contiguous()
+        a.g_raw = gr.data_ptr()
+        g_pts = torch.empty_like(pts) if need[1] else None
+        a.g_pts = _ptr(g_pts)
+        grid_grads = [None] * 4
+        for k in plan.grids:
+            a.grids[k].grad = None
+            if need[2 + k]:
+                gg = torch.zeros_like(ctx.grids[k])
+                st = gg.stride()
+                a.grids[k].grad = gg.data_ptr()
+                for ax in range(4):
+                    a.grids[k].grad_stride[ax] = st[1 + ax]
+                grid_grads[k] = gg
+        needs_params = need[6:]
+        flats = _alloc_param_grads(lib, plan, needs_params, a, device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        L.check(lib.nc_points_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
+                "nc_points_backward")
+        pg = _split_param_grads(plan, flats, needs_params)
+        gp = g_pts.to(ctx.p_dtype).reshape(ctx.p_shape) if g_pts is not None else None
+        return (None, gp, *grid_grads, *pg)
+
+
+def make_plan(stage, decoders) -> _Plan:
+    s = L.STAGES[stage] if isinstance(stage, str) else int(stage)
+    return _Plan(s, decoders)

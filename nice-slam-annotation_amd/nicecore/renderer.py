@@ -1,0 +1,94 @@
+"""Drop-in ``Renderer`` (src/utils/Renderer.py:5-341) on the MI355X render core.
+
+Same constructor, attributes and method signatures as the reference, so
+src/Tracker.py / src/Mapper.py / src/utils/Visualizer.py call it unchanged:
+
+  render_batch_ray(c, decoders, rays_d, rays_o, device, stage, gt_depth=None)
+      -> (depth f64 [N], uncertainty f64 [N], color f32 [N,3])      Renderer.py:95
+  eval_points(p, decoders, c=None, stage='color', device='cuda:0')
+      -> raw [P,4]                                                    Renderer.py:36
+  render_img(c, decoders, c2w, device, stage, gt_depth=None)
+      -> (depth [H,W], uncertainty [H,W], color [H,W,3])              Renderer.py:264
+
+Only the configuration the NICE configs use is implemented (N_importance = 0,
+lindisp = False, perturb = 0, occupancy = True; configs/nice_slam.yaml:5,121-126);
+anything else raises instead of silently falling back.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from .ops import eval_points as _eval_points
+from .ops import render_rays
+
+
+class Renderer(object):
+    def __init__(self, cfg, args, slam, points_batch_size=500000, ray_batch_size=100000):
+        self.ray_batch_size = ray_batch_size
+        self.points_batch_size = points_batch_size
+        r = cfg['rendering']
+        self.lindisp = r['lindisp']
+        self.perturb = r['perturb']
+        self.N_samples = r['N_samples']
+        self.N_surface = r['N_surface']
+        self.N_importance = r['N_importance']
+        self.scale = cfg['scale']
+        self.occupancy = cfg['occupancy']
+        self.nice = slam.nice
+        self.bound = slam.bound
+        self.H, self.W, self.fx, self.fy, self.cx, self.cy = (
+            slam.H, slam.W, slam.fx, slam.fy, slam.cx, slam.cy)
+
+    def _check_supported(self):
+        if not self.nice:
+            raise NotImplementedError("nicecore renders NICE decoders only (iMAP* is out of scope)")
+        if self.N_importance > 0 or self.lindisp or self.perturb > 0. or not self.occupancy:
+            raise NotImplementedError(
+                "nicecore implements N_importance=0, lindisp=False, perturb=0, occupancy=True")
+
+    def eval_points(self, p, decoders, c=None, stage='color', device='cuda:0'):
+        """Renderer.py:36-93: NICE.forward plus the strict in-bound mask; points outside
+        the renderer bound get raw[:, 3] = 100."""
+        self._check_supported()
+        outs = []
+        b = self.bound
+        for pi in torch.split(p, self.points_batch_size):
+            m = ((pi[:, 0] < b[0][1]) & (pi[:, 0] > b[0][0]) & (pi[:, 1] < b[1][1]) &
+                 (pi[:, 1] > b[1][0]) & (pi[:, 2] < b[2][1]) & (pi[:, 2] > b[2][0]))
+            raw = _eval_points(decoders, pi, c, stage)
+            occ = torch.where(m, raw[:, 3], torch.full_like(raw[:, 3], 100.0))
+            outs.append(torch.cat([raw[:, :3], occ[:, None]], dim=1))
+        return torch.cat(outs, dim=0)
+
+    def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None,
+                         depth_max=None):
+        """Renderer.py:95-262.  ``depth_max`` (extension) overrides the batch-global
+        max(gt_depth) with a precomputed (e.g. all-reduced) device scalar."""
+        self._check_supported()
+        if gt_depth is not None:
+            gt_depth = gt_depth.reshape(-1)
+        return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
+                           self.N_samples, self.N_surface, depth_max)
+
+    def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
+        """Renderer.py:264-340: chunked full-image render, no grad."""
+        with torch.no_grad():
+            H, W = self.H, self.W
+            i, j = torch.meshgrid(torch.linspace(0, W - 1, W), torch.linspace(0, H - 1, H),
+                                  indexing='ij')
+            i, j = i.t(), j.t()
+            dirs = torch.stack([(i - self.cx) / self.fx, -(j - self.cy) / self.fy,
+                                -torch.ones_like(i)], -1).to(device)
+            c2w = torch.as_tensor(c2w, device=device)
+            rays_d = torch.sum(dirs[..., None, :] * c2w[:3, :3], -1).reshape(-1, 3).float()
+            rays_o = c2w[:3, -1].expand(rays_d.shape).reshape(-1, 3).float()
+            gt = gt_depth.reshape(-1) if gt_depth is not None else None
+            dl, ul, cl = [], [], []
+            for s in range(0, rays_d.shape[0], self.ray_batch_size):
+                d, u, col = self.render_batch_ray(
+                    c, decoders, rays_d[s:s + self.ray_batch_size], rays_o[s:s + self.ray_batch_size],
+                    device, stage, gt_depth=None if gt is None else gt[s:s + self.ray_batch_size])
+                dl.append(d.double()); ul.append(u.double()); cl.append(col)
+            return (torch.cat(dl).reshape(H, W), torch.cat(ul).reshape(H, W),
+                    torch.cat(cl).reshape(H, W, 3))

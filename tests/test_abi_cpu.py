@@ -1,0 +1,66 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the
+header declares, the ctypes mirror matches the C struct layout, and the flat
+parameter counts match the decoder modules."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+from nicecore import _lib as L
+from nicecore import build as B
+from nicecore import decoder as D
+from nicecore.render_fn import decoder_params
+
+
+@pytest.fixture(scope="module")
+def lib():
+    B.build()
+    return L.load()
+
+
+def declared_symbols():
+    hdr = open(os.path.join(REPO, "include", "nicecore.h")).read()
+    return sorted(set(re.findall(r"\b(nc_[a-z_]+)\s*\(", hdr)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(L.EXPORTS)
+
+
+def test_every_declared_symbol_is_exported(lib):
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_struct_layouts_match(lib):
+    assert lib.nc_struct_size(0) == ctypes.sizeof(L.NcRenderArgs)
+    assert lib.nc_struct_size(1) == ctypes.sizeof(L.NcPointsArgs)
+    assert lib.nc_struct_size(2) == ctypes.sizeof(L.NcGrid)
+    assert lib.nc_struct_size(3) == ctypes.sizeof(L.NcDecoderParams)
+    assert lib.nc_abi_version() == L.NC_ABI_VERSION
+
+
+def test_param_counts_match_modules(lib):
+    m = D.build_default_nice(seed=0)
+    mods = [m.coarse_decoder, m.middle_decoder, m.fine_decoder, m.color_decoder]
+    total = 0
+    for k, mod in enumerate(mods):
+        ps = decoder_params(mod, k)
+        assert [id(p) for p in ps] == [id(p) for p in mod.parameters()]  # flat order == parameters()
+        n = sum(p.numel() for p in ps)
+        assert lib.nc_param_count(k) == n
+        total += n
+    assert total == 58956
+
+
+def test_bad_args_fail_loudly(lib):
+    a = L.NcRenderArgs()
+    a.abi_version = 999
+    assert lib.nc_render_workspace_bytes(ctypes.byref(a)) == 0
+    assert b"ABI" in lib.nc_last_error()
+    a.abi_version = L.NC_ABI_VERSION
+    a.stage = 7
+    assert lib.nc_render_forward(ctypes.byref(a), None, 0, None) < 0
+    assert b"stage" in lib.nc_last_error()
