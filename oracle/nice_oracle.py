@@ -16,8 +16,25 @@ Every function cites the reference lines it restates.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.nn.functional as F
+
+# Compute dtype of the reference's float32 stages.  The reference is float32
+# (FLOAT = torch.float32); tests switch it to float64 with ``float64_mode()`` to
+# obtain a ground truth against which both fp32 implementations are scored.
+FLOAT = torch.float32
+
+
+@contextlib.contextmanager
+def float64_mode():
+    global FLOAT
+    old, FLOAT = FLOAT, torch.float64
+    try:
+        yield
+    finally:
+        FLOAT = old
 
 STAGE_DECODERS = {  # decoder.py:341-370 (which MLPs feed raw at each stage)
     "coarse": ("coarse",),
@@ -36,7 +53,7 @@ def normalize_3d_coordinate(p: torch.Tensor, bound: torch.Tensor) -> torch.Tenso
 def sample_grid_feature(p: torch.Tensor, grid: torch.Tensor, bound: torch.Tensor) -> torch.Tensor:
     """decoder.py:179-188 — trilinear (mode 'bilinear' on 5-D), border padding,
     align_corners=True.  Returns [P, C]."""
-    vgrid = normalize_3d_coordinate(p, bound).unsqueeze(0)[:, :, None, None].float()
+    vgrid = normalize_3d_coordinate(p, bound).unsqueeze(0)[:, :, None, None].to(FLOAT)
     c = F.grid_sample(grid, vgrid, padding_mode='border', align_corners=True, mode='bilinear')
     return c.squeeze(-1).squeeze(-1).transpose(1, 2).squeeze(0)
 
@@ -52,7 +69,7 @@ def mlp_forward(p, grids, prm, pre, name, bound, color=False, concat=False):
         with torch.no_grad():
             c_mid = sample_grid_feature(p, grids['grid_middle'], bound)
         c = torch.cat([c, c_mid], dim=1)
-    pf = p.float()
+    pf = p.to(FLOAT)
     emb = torch.sin(pf @ prm[pre + 'embedder._B'])  # decoder.py:26-30
     h = emb
     for i in range(5):
@@ -80,17 +97,17 @@ def nice_forward(p, grids, prm, dec_bounds, stage):
     P = p.shape[0]
     if stage == 'coarse':
         occ = mlp_no_xyz_forward(p, grids, prm, 'coarse_decoder.', dec_bounds['coarse'])
-        raw = torch.zeros(P, 4, dtype=torch.float32)
+        raw = torch.zeros(P, 4, dtype=FLOAT)
         raw[..., -1] = occ
         return raw
     if stage == 'middle':
         occ = mlp_forward(p, grids, prm, 'middle_decoder.', 'middle', dec_bounds['middle'])
-        raw = torch.zeros(P, 4, dtype=torch.float32)
+        raw = torch.zeros(P, 4, dtype=FLOAT)
         raw[..., -1] = occ
         return raw
     fine_occ = mlp_forward(p, grids, prm, 'fine_decoder.', 'fine', dec_bounds['fine'], concat=True)
     if stage == 'fine':
-        raw = torch.zeros(P, 4, dtype=torch.float32)
+        raw = torch.zeros(P, 4, dtype=FLOAT)
     else:
         raw = mlp_forward(p, grids, prm, 'color_decoder.', 'color', dec_bounds['color'], color=True)
     mid_occ = mlp_forward(p, grids, prm, 'middle_decoder.', 'middle', dec_bounds['middle'])
@@ -109,8 +126,9 @@ def eval_points(p, grids, prm, bound, dec_bounds, stage):
     return ret
 
 
-def sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf):
-    """Renderer.py:116-224 — z_vals [N, S] float64 (stratified + surface, sorted)."""
+def sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf, depth_max=None):
+    """Renderer.py:116-224 — z_vals [N, S] float64 (stratified + surface, sorted).
+    ``depth_max`` (sharding tests only) replaces the batch-global max(gt_depth)."""
     N = rays_o.shape[0]
     if gt_depth is None:
         n_surf = 0
@@ -124,14 +142,17 @@ def sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf):
         t = (bound.unsqueeze(0) - o) / d
         far_bb, _ = torch.min(torch.max(t, dim=2)[0], dim=1)
         far_bb = far_bb.unsqueeze(-1) + 0.01
-    far = torch.clamp(far_bb, 0, torch.max(gt_depth * 1.2)) if gt_depth is not None else far_bb
+    gmax = None
+    if gt_depth is not None:
+        gmax = torch.max(gt_depth) if depth_max is None else depth_max.reshape(())
+    far = torch.clamp(far_bb, 0, gmax * 1.2) if gt_depth is not None else far_bb
     if n_surf > 0:
         pos = gt_depth > 0
         ts = torch.linspace(0., 1., steps=n_surf).double()
         zs = torch.zeros(N, n_surf).double()
         g = gt_depth[pos].unsqueeze(-1).repeat(1, n_surf)
         zs[pos.squeeze(-1), :] = 0.95 * g * (1. - ts) + 1.05 * g * ts
-        zs[~pos.squeeze(-1), :] = 0.001 * (1. - ts) + torch.max(gt_depth) * ts
+        zs[~pos.squeeze(-1), :] = 0.001 * (1. - ts) + gmax * ts
     tv = torch.linspace(0., 1., steps=n_strat)
     z = near * (1. - tv) + far * tv
     if n_surf > 0:
@@ -144,8 +165,8 @@ def composite(raw, z_vals):
     cumprod of (1-alpha+1e-10); rgb, depth (f64) and depth variance (f64)."""
     rgb = raw[..., :-1]
     alpha = torch.sigmoid(10 * raw[..., -1])
-    ones = torch.ones((alpha.shape[0], 1), dtype=torch.float32)
-    weights = alpha.float() * torch.cumprod(torch.cat([ones, (1. - alpha + 1e-10).float()], -1), -1)[:, :-1]
+    ones = torch.ones((alpha.shape[0], 1), dtype=FLOAT)
+    weights = alpha.to(FLOAT) * torch.cumprod(torch.cat([ones, (1. - alpha + 1e-10).to(FLOAT)], -1), -1)[:, :-1]
     rgb_map = torch.sum(weights[..., None] * rgb, -2)
     depth_map = torch.sum(weights * z_vals, -1)
     tmp = z_vals - depth_map.unsqueeze(-1)
@@ -154,12 +175,12 @@ def composite(raw, z_vals):
 
 
 def render_batch_ray(grids, prm, dec_bounds, bound, rays_d, rays_o, stage, gt_depth=None,
-                     n_strat=32, n_surf=16):
+                     n_strat=32, n_surf=16, depth_max=None):
     """Renderer.py:95-262 (N_importance = 0, lindisp/perturb off, occupancy on).
     Returns (depth f64 [N], uncertainty f64 [N], color f32 [N,3])."""
     if stage == 'coarse':
         gt_depth = None
-    z = sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf)
+    z = sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf, depth_max)
     S = z.shape[1]
     pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
     raw = eval_points(pts.reshape(-1, 3), grids, prm, bound, dec_bounds, stage)

@@ -89,3 +89,51 @@ def compare(rec, got):
         else:
             out[k] = float(v.abs().max())  # reference has no gradient here -> must be ~0
     return out
+
+
+def oracle_render_grads(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, f64=False):
+    """CPU oracle render + backward; with f64=True everything runs in float64
+    (ground truth).  Returns {name: tensor} like run_case."""
+    from oracle import nice_oracle as O
+    cast = (lambda t: t.double()) if f64 else (lambda t: t)
+    ro_c = cast(ro.clone()).requires_grad_(True)
+    rd_c = cast(rd.clone()).requires_grad_(True)
+    g_c = {k: cast(v.clone()).requires_grad_(True) for k, v in grids.items()}
+    prm_c = {k: cast(v.clone()).requires_grad_(True) for k, v in params.items()}
+    gt_c = cast(gt) if gt is not None else None
+    ctx = O.float64_mode() if f64 else _null()
+    with ctx:
+        d, v, c = O.render_batch_ray(g_c, prm_c, dec_b, bound, rd_c, ro_c, stage, gt_c)
+        gd, gv, gc = upstream
+        torch.autograd.backward([d, v, c], [gd, gv, cast(gc)])
+    out = {"depth": d.detach(), "var": v.detach(), "color": c.detach(),
+           "grad/rays_o": ro_c.grad, "grad/rays_d": rd_c.grad}
+    for k, t in g_c.items():
+        if t.grad is not None and float(t.grad.abs().max()) > 0:
+            out["grad/" + k] = t.grad
+    for k, t in prm_c.items():
+        if t.grad is not None and float(t.grad.abs().max()) > 0:
+            out["grad/param/" + k] = t.grad
+    return out
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def score_vs_truth(got, ref32, ref64, out_floor=2e-5, grad_floor=2e-4):
+    """{name: (err_hip, err_ref32, allowed)} where err = scale-aware error vs float64."""
+    res = {}
+    for k, t64 in ref64.items():
+        if k not in got:
+            res[k] = (float("inf"), 0.0, 0.0)
+            continue
+        e_hip = rel_err(got[k], t64)
+        e_ref = rel_err(ref32[k], t64) if k in ref32 else 0.0
+        floor = grad_floor if k.startswith("grad/") else out_floor
+        res[k] = (e_hip, e_ref, max(4.0 * e_ref, floor))
+    return res

@@ -1,0 +1,112 @@
+"""Ray-sharded data parallelism (nicecore.distributed) on 2 gloo ranks.
+
+Each rank renders its contiguous shard of the batch with the CPU oracle, using
+the all-reduced batch-global depth max, back-propagates the mapper loss and
+all-reduces grid + decoder gradients.  The summed gradients and the gathered ray
+gradients must equal a single-process render of the whole batch.  Also shows why
+the MAX pre-reduce is required: without it outputs change."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import load_case, load_scene
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _render_loss(O, grids, prm, bound, cbound, ro, rd, dep, col, depth_max=None):
+    dec_b = {"coarse": cbound, "middle": bound, "fine": bound, "color": bound}
+    d, u, c = O.render_batch_ray(grids, prm, dec_b, bound, rd, ro, "color", dep, depth_max=depth_max)
+    loss = ((dep.double() - d).abs() * (dep > 0).double()).sum() + 0.2 * (col - c).abs().sum()
+    return loss, d
+
+
+def _worker(rank, world, port, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import conftest  # noqa: F401  (paths)
+    from oracle import nice_oracle as O
+    from nicecore import distributed as ND
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    bound, cbound, grids, params = load_scene()
+    rec = load_case("color_depth")
+    ro, rd, dep, col = ND.shard(rank, world, rec["rays_o"], rec["rays_d"], rec["gt_depth"], rec["gt_color"])
+    ro = ro.clone().requires_grad_(True)
+    rd = rd.clone().requires_grad_(True)
+    g = {k: v.clone().requires_grad_(True) for k, v in grids.items()}
+    prm = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    dmax = ND.global_depth_max(dep)
+    loss, _ = _render_loss(O, g, prm, bound, cbound, ro, rd, dep, col, depth_max=dmax)
+    loss.backward()
+    ND.allreduce_grads(list(g.values()) + list(prm.values()))
+    gro = [torch.zeros(0)] * world
+    sizes = [ND.shard_bounds(rec["rays_o"].shape[0], r, world) for r in range(world)]
+    gathered = [torch.zeros(b - a, 3) for a, b in sizes]
+    dist.all_gather(gathered, ro.grad.contiguous())
+    if rank == 0:
+        # numpy copies: torch tensors in an mp.Queue share fds that die with this process
+        out.put({"grids": {k: v.grad.numpy().copy() for k, v in g.items() if v.grad is not None},
+                 "params": {k: v.grad.numpy().copy() for k, v in prm.items() if v.grad is not None},
+                 "rays_o": torch.cat(gathered).numpy().copy()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_grads_equal_full_batch():
+    from oracle import nice_oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    bound, cbound, grids, params = load_scene()
+    rec = load_case("color_depth")
+    ro = rec["rays_o"].clone().requires_grad_(True)
+    rd = rec["rays_d"].clone().requires_grad_(True)
+    g = {k: v.clone().requires_grad_(True) for k, v in grids.items()}
+    prm = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    loss, _ = _render_loss(O, g, prm, bound, cbound, ro, rd, rec["gt_depth"], rec["gt_color"])
+    loss.backward()
+    for k, v in res["grids"].items():
+        torch.testing.assert_close(torch.from_numpy(v), g[k].grad, rtol=1e-5, atol=1e-7)
+    for k, v in res["params"].items():
+        torch.testing.assert_close(torch.from_numpy(v), prm[k].grad, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.from_numpy(res["rays_o"]), ro.grad, rtol=1e-6, atol=1e-7)
+
+
+def test_local_depth_max_changes_outputs():
+    """Rendering a shard with its LOCAL max(gt_depth) is not the reference result."""
+    from oracle import nice_oracle as O
+    from nicecore import distributed as ND
+    bound, cbound, grids, params = load_scene()
+    rec = load_case("color_depth")
+    dec_b = {"coarse": cbound, "middle": bound, "fine": bound, "color": bound}
+    full, _, _ = O.render_batch_ray(grids, params, dec_b, bound, rec["rays_d"], rec["rays_o"], "color",
+                                    rec["gt_depth"])
+    ro, rd, dep = ND.shard(1, 2, rec["rays_o"], rec["rays_d"], rec["gt_depth"])
+    a, b = ND.shard_bounds(rec["rays_o"].shape[0], 1, 2)
+    local, _, _ = O.render_batch_ray(grids, params, dec_b, bound, rd, ro, "color", dep)
+    glob, _, _ = O.render_batch_ray(grids, params, dec_b, bound, rd, ro, "color", dep,
+                                    depth_max=rec["gt_depth"].max())
+    torch.testing.assert_close(glob, full[a:b], rtol=0, atol=0)
+    if float(dep.max()) != float(rec["gt_depth"].max()):
+        assert float((local - full[a:b]).abs().max()) > 0

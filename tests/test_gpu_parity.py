@@ -130,8 +130,12 @@ def _room0_case(n_rays, stage, seed=7):
 @pytest.mark.gpu
 @pytest.mark.parametrize("stage", ["color", "middle"])
 def test_room0_against_oracle(stage):
-    """Benchmark geometry (Replica room0 bound and grid shapes), 256 rays, HIP vs CPU oracle."""
-    from oracle import nice_oracle as O
+    """Benchmark geometry (Replica room0 bound and grid shapes), 256 rays.  Scored
+    against a float64 ground truth: the HIP error must stay within 4x the fp32
+    reference's own error (floors 2e-5 outputs / 2e-4 gradients) -- gradient
+    reductions over thousands of points cancel, so a plain relative bound is the
+    wrong metric there."""
+    from parity_common import oracle_render_grads, score_vs_truth
     sc, grids, params, ro, rd, dep = _room0_case(256, stage)
     cb = sc.bound * 2
     dec_b = {"coarse": cb, "middle": sc.bound, "fine": sc.bound, "color": sc.bound}
@@ -140,12 +144,8 @@ def test_room0_against_oracle(stage):
     gd = torch.randn(ro.shape[0], generator=gen, dtype=torch.float64)
     gv = torch.randn(ro.shape[0], generator=gen, dtype=torch.float64)
     gc = torch.randn(ro.shape[0], 3, generator=gen)
-    # oracle
-    ro_c, rd_c = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
-    g_c = {k: v.clone().requires_grad_(True) for k, v in grids.items()}
-    prm_c = {k: v.clone().requires_grad_(True) for k, v in params.items()}
-    d_c, v_c, c_c = O.render_batch_ray(g_c, prm_c, dec_b, sc.bound, rd_c, ro_c, stage, gt)
-    torch.autograd.backward([d_c, v_c, c_c], [gd, gv, gc])
+    ref32 = oracle_render_grads(grids, params, dec_b, sc.bound, ro, rd, stage, gt, (gd, gv, gc))
+    ref64 = oracle_render_grads(grids, params, dec_b, sc.bound, ro, rd, stage, gt, (gd, gv, gc), f64=True)
     # HIP (channels-last grids, the fast layout)
     model = build_model(params, sc.bound, cb, "cuda")
     ro_g, rd_g = ro.cuda().requires_grad_(True), rd.cuda().requires_grad_(True)
@@ -155,19 +155,17 @@ def test_room0_against_oracle(stage):
     d_g, v_g, c_g = r.render_batch_ray(g_g, model, rd_g, ro_g, "cuda", stage,
                                        gt.cuda() if gt is not None else None)
     torch.autograd.backward([d_g, v_g, c_g], [gd.cuda(), gv.cuda(), gc.cuda()])
-    assert rel_err(d_g.detach().cpu(), d_c.detach()) <= OUT_TOL
-    assert rel_err(v_g.detach().cpu(), v_c.detach()) <= OUT_TOL
-    assert rel_err(c_g.detach().cpu(), c_c.detach()) <= OUT_TOL
-    assert rel_err(ro_g.grad.cpu(), ro_c.grad) <= GRAD_TOL
-    assert rel_err(rd_g.grad.cpu(), rd_c.grad) <= GRAD_TOL
+    got = {"depth": d_g.detach().cpu(), "var": v_g.detach().cpu(), "color": c_g.detach().cpu(),
+           "grad/rays_o": ro_g.grad.cpu(), "grad/rays_d": rd_g.grad.cpu()}
     for k, v in g_g.items():
-        ref = g_c[k].grad
-        if ref is not None and float(ref.abs().max()) > 0:
-            assert rel_err(v.grad.cpu(), ref) <= GRAD_TOL, k
+        if v.grad is not None:
+            got["grad/" + k] = v.grad.cpu()
     for n, p in model.named_parameters():
-        ref = prm_c[n].grad
-        if ref is not None and float(ref.abs().max()) > 0:
-            assert rel_err(p.grad.cpu(), ref) <= GRAD_TOL, n
+        if p.grad is not None:
+            got["grad/param/" + n] = p.grad.cpu()
+    scores = score_vs_truth(got, ref32, ref64)
+    bad = {k: v for k, v in scores.items() if not v[0] <= v[2]}
+    assert not bad, bad
 
 
 @pytest.mark.gpu
