@@ -34,11 +34,11 @@ int check_hip(int e, const char* what) {
 // ---- optional per-kernel event timing (nc_timing_start / nc_timing_stop) ----
 enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_BWD,
-  KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_COUNT
+  KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_bwd", "k_param_reduce", "k_ray_grads",
-                                       "k_points_assemble", "k_points_split_grad", "k_points_grads"};
+                                       "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -141,7 +141,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, z = 0, pts = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, total = 0;
+  size_t dmax = 0, z = 0, pts = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, total = 0;
   int slab_wgs = 1;
   int64_t slab_stride = 0;
 };
@@ -161,6 +161,7 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, Ws& w) {
   w.gocc = take((size_t)P * 4);
   w.grgb = take((size_t)P * 12);
   w.dpts = take((size_t)pl.n_jobs * P * 24);
+  w.dcbuf = take((size_t)pl.n_jobs * P * 32 * 4);
   const int64_t blocks = (P + 63) / 64;
   int per_job = (cu_count() + pl.n_jobs - 1) / pl.n_jobs;
   if (per_job < 1) per_job = 1;
@@ -198,6 +199,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.gocc = at<float>(ws, w.gocc);
   m.grgb = at<float>(ws, w.grgb);
   m.dpts = at<double>(ws, w.dpts);
+  m.dcbuf = at<float>(ws, w.dcbuf);
   m.slab = at<float>(ws, w.slab);
 }
 
@@ -208,7 +210,7 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   if (a->n_rays < 0) return fail(-1, "nicecore: n_rays < 0");
   if (a->n_strat < 1 || a->n_surf < 0 || a->n_surf > NC_MAX_SURF || a->n_strat + a->n_surf > NC_MAX_SAMPLES)
     return fail(-1, "nicecore: need 1 <= N_samples, 0 <= N_surface <= 32, N_samples + N_surface <= 64");
-  if (a->n_surf > 0 && !a->gt_depth) return fail(-1, "nicecore: N_surface > 0 requires gt_depth");
+  if (a->n_surf > 0 && !a->gt_depth && a->n_rays > 0) return fail(-1, "nicecore: N_surface > 0 requires gt_depth");
   if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
   S = a->n_strat + a->n_surf;
   P = a->n_rays * S;
@@ -390,6 +392,7 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   if (!any) return 0;
   if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
   if (int e = check_hip(timed(KID_MLP_BWD, s, [&] { return launch_mlp_bwd(m, s); }), "k_mlp_bwd")) return e;
+  if (int e = check_hip(timed(KID_GRID_BWD, s, [&] { return launch_grid_bwd(m, s); }), "k_grid_bwd")) return e;
   if (int e = reduce_params(m, a->dec, s)) return e;
   if (need_coord)
     if (int e = check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(rc, s); }), "k_ray_grads")) return e;
@@ -441,6 +444,7 @@ int nc_points_backward(const nc_points_args* a, void* ws, size_t ws_bytes, void*
   if (int e = check_hip(timed(KID_POINTS_SPLIT, s, [&] { return launch_points_split_grad(m, a->stage, a->g_raw, (float*)m.gocc, (float*)m.grgb, s); }), "k_points_split_grad"))
     return e;
   if (int e = check_hip(timed(KID_MLP_BWD, s, [&] { return launch_mlp_bwd(m, s); }), "k_mlp_bwd")) return e;
+  if (int e = check_hip(timed(KID_GRID_BWD, s, [&] { return launch_grid_bwd(m, s); }), "k_grid_bwd")) return e;
   if (int e = reduce_params(m, a->dec, s)) return e;
   if (a->g_pts)
     if (int e = check_hip(timed(KID_POINTS_GRADS, s, [&] { return launch_points_grads(m, a->g_pts, s); }), "k_points_grads")) return e;

@@ -35,6 +35,7 @@ struct MlpCtx {
   const float* gocc;         // [P] d loss / d occupancy (shared by the occupancy decoders)
   const float* grgb;         // [P][3] d loss / d rgb
   double* dpts;              // [n_jobs][P][3] per-decoder point gradients
+  float* dcbuf;              // [n_jobs][P][32] d loss / d own-grid features (k_mlp_bwd -> k_grid_bwd)
   float* slab;               // [n_jobs][slab_wgs][slab_stride] per-workgroup parameter gradients
   int64_t slab_stride;
 };
@@ -99,6 +100,7 @@ int mlp_fwd_lds_bytes();
 int mlp_bwd_lds_bytes();
 int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_bwd(const MlpCtx& c, hipStream_t s);
+int launch_grid_bwd(const MlpCtx& c, hipStream_t s);
 int64_t max_param_count();
 
 constexpr int FWD_THREADS = 512;  // 8 waves, 128 points per workgroup iteration

@@ -282,10 +282,12 @@ __global__ void __launch_bounds__(FWD_THREADS) k_mlp_fwd(const MlpCtx ctx) {
 constexpr int CH = 64;  // points per sub-chunk (4 waves x 16)
 
 // dW[16*to + r][16*ti + c] += sum over the 64 staged points of Y[pt][.] X[pt][.]
-// Tiles tau = wave + 4*s (s < NS) of an NR x NC tile grid; bias row-sums in bsum.
+// Tiles tau = wave + 4*s (s < NS) of an NR x NC tile grid.  With BIAS, the owner
+// of a first-column tile also adds the row sums of Y (the bias gradient) into the
+// LDS accumulator bacc[16*to + r].
 template <int NR, int NC, int NS, bool BIAS>
 __device__ __forceinline__ void dw_phase(const float* Y, int ldY, const float* X, int ldX, floatx4* acc,
-                                         float* bsum, int wave, int i, int g) {
+                                         float* bacc, int wave, int i, int g) {
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int tau = wave + 4 * s;
@@ -302,7 +304,10 @@ __device__ __forceinline__ void dw_phase(const float* Y, int ldY, const float* X
         if (BIAS) bs += av;
       }
       acc[s] = a;
-      if (BIAS && ti == 0) bsum[s] += bs;
+      if (BIAS && ti == 0) {
+        bs = sum_groups(bs);
+        if (g == 0) atomicAdd(bacc + 16 * to + i, bs);
+      }
     }
   }
 }
@@ -343,8 +348,7 @@ struct PhaseMap {
 };
 
 template <int KIND, int NR, int NC, int NS>
-__device__ __forceinline__ void flush_phase(float* img, int ph, const floatx4* acc, const float* bsum,
-                                            int wave, int i, int g) {
+__device__ __forceinline__ void flush_phase(float* img, int ph, const floatx4* acc, int wave, int i, int g) {
   using PM = PhaseMap<KIND>;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -355,11 +359,6 @@ __device__ __forceinline__ void flush_phase(float* img, int ph, const floatx4* a
       for (int r = 0; r < 4; ++r) {
         const int64_t idx = PM::w_index(ph, 16 * to + 4 * g + r, 16 * ti + i);
         if (idx >= 0) atomicAdd(img + idx, acc[s][r]);
-      }
-      float b = sum_groups(bsum[s]);
-      if (ti == 0 && g == 0) {
-        const int64_t bi = PM::b_index(ph, 16 * to + i);
-        if (bi >= 0) atomicAdd(img + bi, b);
       }
     }
   }
@@ -400,7 +399,11 @@ struct BwdLds {
   static constexpr int CBUF = N::WEIGHTS;
   static constexpr int STAGE = CBUF + (N::XYZ ? CH * LDCB : 0);
   static constexpr int STAGE_FLOATS = CH * (48 + 144);
-  static constexpr int TOTAL = STAGE + STAGE_FLOATS;
+  static constexpr int BACC = STAGE + STAGE_FLOATS;  // bias-gradient accumulators
+  // per phase id (see PhaseMap): 0 out (16), 1..5 pts_linears[4..0] (32 each), 6..10 fc_c[4..0]
+  __host__ __device__ static constexpr int bacc_off(int ph) { return ph == 0 ? 0 : 16 + 32 * (ph - 1); }
+  static constexpr int BACC_FLOATS = 16 + 32 * 10;
+  static constexpr int TOTAL = BACC + BACC_FLOATS;
 };
 
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -409,45 +412,6 @@ constexpr int BWD_LDS_FLOATS =
 constexpr int FWD_LDS_FLOATS =
     cmax(cmax(Net<K_COARSE>::WEIGHTS, Net<K_MID>::WEIGHTS), cmax(Net<K_FINE>::WEIGHTS, Net<K_COLOR>::WEIGHTS));
 static_assert(BWD_LDS_FLOATS * 4 <= 160 * 1024, "backward LDS budget");
-
-// trilinear backward of one lookup: grid-gradient scatter + coordinate gradient
-template <bool VEC>
-__device__ __forceinline__ void grid_backward(const nc_grid& G, const Corners& c, const float dc[8], int g,
-                                              bool want_grid, bool want_coord, float gi[3]) {
-  gi[0] = gi[1] = gi[2] = 0.f;
-  const int64_t sC = G.stride[0];
-  const int64_t gC = G.grad_stride[0];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (!((c.inb >> k) & 1u)) continue;
-    const int xb = k & 1, yb = (k >> 1) & 1, zb = k >> 2;
-    if (want_coord) {
-      const float* base = G.data + c.off[k];
-      float v[8];
-      if (VEC) {
-        const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
-        const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = base[(int64_t)feat_of(j, g) * sC];
-      }
-      float dot = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dot = dot + v[j] * dc[j];
-      gi[0] = gi[0] + (xb ? dot : -dot) * c.wy[yb] * c.wz[zb];
-      gi[1] = gi[1] + (yb ? dot : -dot) * c.wx[xb] * c.wz[zb];
-      gi[2] = gi[2] + (zb ? dot : -dot) * c.wx[xb] * c.wy[yb];
-    }
-    if (want_grid) {
-      float* gbase = G.grad + (c.z0 + zb) * G.grad_stride[1] + (c.y0 + yb) * G.grad_stride[2] +
-                     (c.x0 + xb) * G.grad_stride[3];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(gbase + (int64_t)feat_of(j, g) * gC, c.w[k] * dc[j]);
-    }
-  }
-}
 
 template <int KIND>
 __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float* lds) {
@@ -465,12 +429,11 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
   const bool need_dc = need_grid || need_coord;
 
   floatx4 acc[SL::TOTAL];
-  float bsum[SL::TOTAL];
 #pragma unroll
-  for (int s = 0; s < SL::TOTAL; ++s) {
-    acc[s] = zero4();
-    bsum[s] = 0.f;
-  }
+  for (int s = 0; s < SL::TOTAL; ++s) acc[s] = zero4();
+  float* bacc = lds + BL::BACC;
+  for (int e = threadIdx.x; e < BL::BACC_FLOATS; e += blockDim.x) bacc[e] = 0.f;
+  __syncthreads();
 
   const int64_t nblk = (ctx.P + CH - 1) / CH;
   for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
@@ -508,7 +471,7 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
       stage_rows<2>(X, 48, 0, R.h[4], row, g);
       if constexpr (N::XYZ) stage_rows<N::CD / 16>(cbuf, BL::LDCB, 0, R.c, row, g);
       __syncthreads();
-      dw_phase<1, 2, 1, true>(Y, 16, X, 48, acc + SL::OUT, bsum + SL::OUT, wave, i, g);
+      dw_phase<1, 2, 1, true>(Y, 16, X, 48, acc + SL::OUT, bacc + BL::bacc_off(0), wave, i, g);
       __syncthreads();
     }
 
@@ -548,18 +511,18 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
         }
         __syncthreads();
         if (L == 0) {
-          dw_phase<2, SL::NC0, SL::ns(2 * SL::NC0), true>(Y, 48, X, ldx, acc + SL::L0, bsum + SL::L0, wave, i, g);
+          dw_phase<2, SL::NC0, SL::ns(2 * SL::NC0), true>(Y, 48, X, ldx, acc + SL::L0, bacc + BL::bacc_off(5 - L), wave, i, g);
         } else if (L == 3) {
-          dw_phase<2, SL::NC3, SL::ns(2 * SL::NC3), true>(Y, 48, X, ldx, acc + SL::L3, bsum + SL::L3, wave, i, g);
+          dw_phase<2, SL::NC3, SL::ns(2 * SL::NC3), true>(Y, 48, X, ldx, acc + SL::L3, bacc + BL::bacc_off(5 - L), wave, i, g);
         } else {
-          dw_phase<2, 2, 1, true>(Y, 48, X, ldx, acc + SL::lin(L), bsum + SL::lin(L), wave, i, g);
+          dw_phase<2, 2, 1, true>(Y, 48, X, ldx, acc + SL::lin(L), bacc + BL::bacc_off(5 - L), wave, i, g);
         }
         __syncthreads();
         if constexpr (N::XYZ) {
           stage_rows<2>(Y, 48, 0, dh, row, g);
           __syncthreads();
           dw_phase<2, SL::NCC, SL::ns(2 * SL::NCC), true>(Y, 48, cbuf, BL::LDCB, acc + SL::fc(L),
-                                                          bsum + SL::fc(L), wave, i, g);
+                                                          bacc + BL::bacc_off(10 - L), wave, i, g);
           __syncthreads();
         }
       }
@@ -621,44 +584,22 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
         *reinterpret_cast<float4*>(X + row * 16 + 4 * g) =
             g == 0 ? float4{R.pf[0], R.pf[1], R.pf[2], 0.f} : float4{0.f, 0.f, 0.f, 0.f};
         __syncthreads();
-        dw_phase<6, 1, 2, false>(Y, 112, X, 16, acc + SL::FB, bsum + SL::FB, wave, i, g);
+        dw_phase<6, 1, 2, false>(Y, 112, X, 16, acc + SL::FB, nullptr, wave, i, g);
         __syncthreads();
       }
     }
 
-    // trilinear backward into the decoder's own grid + point gradient
-    if (need_dc) {
-      float dcr[8];
+    // hand the trilinear backward to k_grid_bwd: d features (this decoder's own 32
+    // channels, C layout) and the Fourier part of the point gradient
+    if (need_dc && valid) {
+      float* dst = ctx.dcbuf + ((int64_t)job.slot * ctx.P + p) * HID;
+      *reinterpret_cast<float4*>(dst + 4 * g) = float4{dc[0][0], dc[0][1], dc[0][2], dc[0][3]};
+      *reinterpret_cast<float4*>(dst + 16 + 4 * g) = float4{dc[1][0], dc[1][1], dc[1][2], dc[1][3]};
+    }
+    if (need_coord && valid && g == 0) {
+      double* dst = ctx.dpts + ((int64_t)job.slot * ctx.P + p) * 3;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dcr[r] = dc[0][r];
-        dcr[4 + r] = dc[1][r];
-      }
-      const nc_grid& G = ctx.grids[KIND];
-      Corners co;
-      {
-        float xyz[3];
-        normalize_pt(R.p, ctx.dec[KIND].bound, xyz);
-        make_corners(G, xyz, co);
-      }
-      float gi[3];
-      if (grid_vec_ok(G)) grid_backward<true>(G, co, dcr, g, need_grid && valid, need_coord, gi);
-      else grid_backward<false>(G, co, dcr, g, need_grid && valid, need_coord, gi);
-      if (need_coord) {
-        gi[0] = sum_groups(gi[0]) * co.gmx;
-        gi[1] = sum_groups(gi[1]) * co.gmy;
-        gi[2] = sum_groups(gi[2]) * co.gmz;
-        if (valid && g == 0) {
-          const nc_decoder_params& D = ctx.dec[KIND];
-          double* dst = ctx.dpts + ((int64_t)job.slot * ctx.P + p) * 3;
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            // normalize_3d_coordinate backward: (g * 2) / (hi - lo), then + d p.float()
-            const double gg = ((double)gi[k] * 2.0) / (D.bound[k][1] - D.bound[k][0]);
-            dst[k] = gg + (double)dpf[k];
-          }
-        }
-      }
+      for (int k = 0; k < 3; ++k) dst[k] = (double)dpf[k];
     }
   }
 
@@ -668,16 +609,25 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
   float* img = lds;
   for (int e = threadIdx.x; e < N::NPARAM; e += blockDim.x) img[e] = 0.f;
   __syncthreads();
-  flush_phase<KIND, 1, 2, 1>(img, 0, acc + SL::OUT, bsum + SL::OUT, wave, i, g);
+  flush_phase<KIND, 1, 2, 1>(img, 0, acc + SL::OUT, wave, i, g);
 #pragma unroll
   for (int L = 4; L >= 0; --L) {
-    if (L == 0) flush_phase<KIND, 2, SL::NC0, SL::ns(2 * SL::NC0)>(img, 5 - L, acc + SL::L0, bsum + SL::L0, wave, i, g);
-    else if (L == 3) flush_phase<KIND, 2, SL::NC3, SL::ns(2 * SL::NC3)>(img, 5 - L, acc + SL::L3, bsum + SL::L3, wave, i, g);
-    else flush_phase<KIND, 2, 2, 1>(img, 5 - L, acc + SL::lin(L), bsum + SL::lin(L), wave, i, g);
+    if (L == 0) flush_phase<KIND, 2, SL::NC0, SL::ns(2 * SL::NC0)>(img, 5 - L, acc + SL::L0, wave, i, g);
+    else if (L == 3) flush_phase<KIND, 2, SL::NC3, SL::ns(2 * SL::NC3)>(img, 5 - L, acc + SL::L3, wave, i, g);
+    else flush_phase<KIND, 2, 2, 1>(img, 5 - L, acc + SL::lin(L), wave, i, g);
     if constexpr (N::XYZ)
-      flush_phase<KIND, 2, SL::NCC, SL::ns(2 * SL::NCC)>(img, 10 - L, acc + SL::fc(L), bsum + SL::fc(L), wave, i, g);
+      flush_phase<KIND, 2, SL::NCC, SL::ns(2 * SL::NCC)>(img, 10 - L, acc + SL::fc(L), wave, i, g);
   }
-  if constexpr (N::XYZ) flush_phase<KIND, 6, 1, 2>(img, 11, acc + SL::FB, bsum + SL::FB, wave, i, g);
+  if constexpr (N::XYZ) flush_phase<KIND, 6, 1, 2>(img, 11, acc + SL::FB, wave, i, g);
+  // bias gradients from the LDS accumulators
+  for (int e = threadIdx.x; e < BL::BACC_FLOATS; e += blockDim.x) {
+    int ph, row;
+    if (e < 16) { ph = 0; row = e; }
+    else { ph = 1 + (e - 16) / 32; row = (e - 16) % 32; }
+    if (ph > 5 && !N::XYZ) continue;
+    const int64_t bi = PhaseMap<KIND>::b_index(ph, row);
+    if (bi >= 0) img[bi] += bacc[e];
+  }
   __syncthreads();
   float* slab = ctx.slab + ((int64_t)blockIdx.y * ctx.slab_wgs + blockIdx.x) * ctx.slab_stride;
   for (int e = threadIdx.x; e < N::NPARAM; e += blockDim.x) slab[e] = img[e];

@@ -24,9 +24,25 @@ def _ptr(t):
     return t.data_ptr() if t is not None else None
 
 
+_BOUND_CACHE: dict = {}
+
+
 def _bound_rows(b) -> list:
-    b = torch.as_tensor(b).detach().to("cpu", torch.float64).reshape(3, 2)
-    return [[float(b[k, 0]), float(b[k, 1])] for k in range(3)]
+    """[[lo, hi]] * 3 as Python floats.  Device-resident bound tensors are cached by
+    (storage, version) so the per-call path never synchronises on a D2H copy."""
+    if isinstance(b, torch.Tensor):
+        key = (b.data_ptr(), b._version, b.device.type, tuple(b.shape))
+        hit = _BOUND_CACHE.get(key)
+        if hit is not None:
+            return hit
+        t = b.detach().to("cpu", torch.float64).reshape(3, 2)
+        rows = [[float(t[k, 0]), float(t[k, 1])] for k in range(3)]
+        if len(_BOUND_CACHE) > 64:
+            _BOUND_CACHE.clear()
+        _BOUND_CACHE[key] = rows
+        return rows
+    t = torch.as_tensor(b, dtype=torch.float64).reshape(3, 2)
+    return [[float(t[k, 0]), float(t[k, 1])] for k in range(3)]
 
 
 def decoder_modules(decoders):
