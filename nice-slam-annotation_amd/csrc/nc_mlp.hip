@@ -27,6 +27,14 @@
 #include "nc_device.h"
 #include "nc_internal.h"
 
+#ifdef NC_ABL_FAST_TRIG  // timing-only ablation: hardware sin/cos (wrong for large arguments)
+#define NC_SIN __sinf
+#define NC_COS __cosf
+#else
+#define NC_SIN sinf
+#define NC_COS cosf
+#endif
+
 namespace nc {
 
 // ---------------------------------------------------------------------------
@@ -162,7 +170,7 @@ __device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx
       const int m = feat_of(j, g);
       const float x = __builtin_fmaf(R.pf[2], B[2 * EMBP + m],
                                      __builtin_fmaf(R.pf[1], B[EMBP + m], R.pf[0] * B[m]));
-      R.emb[j] = (m < EMB) ? sinf(x) : 0.f;
+      R.emb[j] = (m < EMB) ? NC_SIN(x) : 0.f;
     }
   }
   R.mask_lo = 0;
@@ -566,7 +574,7 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
         const int m = feat_of(j, g);
         const float x = __builtin_fmaf(R.pf[2], B[2 * EMBP + m],
                                        __builtin_fmaf(R.pf[1], B[EMBP + m], R.pf[0] * B[m]));
-        dx[j] = (m < EMB) ? demb[j >> 2][j & 3] * cosf(x) : 0.f;
+        dx[j] = (m < EMB) ? demb[j >> 2][j & 3] * NC_COS(x) : 0.f;
       }
       if (need_coord) {
 #pragma unroll
