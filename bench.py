@@ -36,6 +36,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f3
 HBM_PEAK_GBS = 8000.0
 MAC = {"coarse": 6176, "middle": 15479, "fine": 20599, "color": 15575}  # per point
 TRI_FLOP = 8 * 32 * 2  # one trilinear lookup of 32 channels
+# dX-chain MACs per point: the fine decoder's fc_c input gradient is only taken for its
+# own 32 grid channels (the middle features enter under no_grad, decoder.py:196-202)
+MAC_DX = {"coarse": 6176, "middle": 15479, "fine": 20599 - 5 * 32 * 32, "color": 15575}
 
 
 def parse():
@@ -126,14 +129,16 @@ def make_step(w, args, world, device):
 
 
 def algorithmic_flops_per_ray(stage, S, mode):
+    """Algorithmic FLOP per ray of each decoder kernel:
+    k_mlp_fwd = decoder MACs + trilinear lookups, k_mlp_dx = dX-chain MACs,
+    k_mlp_dw = weight-gradient MACs (BA mode only)."""
     decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
             "color": ["fine", "middle", "color"]}[stage]
     lk_fwd = {"coarse": 1, "middle": 1, "fine": 3, "color": 4}[stage]
-    lk_grad = {"coarse": 1, "middle": 1, "fine": 2, "color": 3}[stage]
-    macs = sum(MAC[d] for d in decs)
-    fwd = 2 * macs + TRI_FLOP * lk_fwd
-    bwd = 2 * macs + 2 * TRI_FLOP * lk_grad + (2 * macs if mode == "ba" else 0)
-    return fwd * S, bwd * S
+    fwd = 2 * sum(MAC[d] for d in decs) + TRI_FLOP * lk_fwd
+    dx = 2 * sum(MAC_DX[d] for d in decs)
+    dw = 2 * sum(MAC[d] for d in decs) if mode == "ba" else 0
+    return {"k_mlp_fwd": fwd * S, "k_mlp_dx": dx * S, "k_mlp_dw": dw * S}
 
 
 def cpu_baseline(args, seconds):
@@ -228,9 +233,8 @@ def main():
     avg_ms = ms_dom / max(n_dom, 1)
 
     S = 48
-    fwd_fl, bwd_fl = algorithmic_flops_per_ray(args.stage, S, args.mode)
-    per_launch = {"k_mlp_fwd": fwd_fl * args.rays, "k_mlp_bwd": bwd_fl * args.rays}
-    fl = per_launch.get(dominant)
+    per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode)
+    fl = per_ray[dominant] * args.rays if dominant in per_ray else None
     roof = None
     if fl is not None and avg_ms > 0:
         ach = fl / (avg_ms * 1e-3) / 1e12

@@ -25,6 +25,10 @@
  *     synchronises the host, so the calls are graph-capturable.
  *   - Return value 0 = success; negative = error (message via nc_last_error(),
  *     thread-local).  No exception crosses this boundary.
+ *   - A backward call needs the forward to have run with NC_SAVE_FOR_BACKWARD in
+ *     `flags` (the forward then keeps each decoder's per-point activations in the
+ *     workspace; the flag also sizes the workspace).  Forward-only callers leave it
+ *     0 and get a much smaller workspace.
  *   - Gradient outputs are ACCUMULATED into for grids (caller zero-fills them) and
  *     OVERWRITTEN for rays and decoder parameters.
  */
@@ -38,9 +42,12 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 1
+#define NC_ABI_VERSION 2
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
+
+/* nc_*_args.flags */
+#define NC_SAVE_FOR_BACKWARD 1
 
 /* Stage names of render_batch_ray / NICE.forward (decoder.py:341-370). */
 enum nc_stage { NC_STAGE_COARSE = 0, NC_STAGE_MIDDLE = 1, NC_STAGE_FINE = 2, NC_STAGE_COLOR = 3 };
@@ -81,6 +88,8 @@ typedef struct nc_render_args {
   int64_t n_rays;
   int32_t n_strat;       /* N_samples (configs/nice_slam.yaml:122) */
   int32_t n_surf;        /* N_surface; must be 0 when gt_depth == NULL or stage == COARSE */
+  int32_t flags;         /* NC_SAVE_FOR_BACKWARD (autograd: the graph requires grad) */
+  int32_t reserved;      /* 0 */
   const float* rays_o;   /* [N,3] */
   const float* rays_d;   /* [N,3] */
   const float* gt_depth; /* [N] or NULL */
@@ -107,6 +116,8 @@ typedef struct nc_points_args {
   int32_t abi_version;
   int32_t stage;
   int64_t n_points;
+  int32_t flags;           /* NC_SAVE_FOR_BACKWARD */
+  int32_t reserved;
   const double* pts;       /* [P,3] float64 (float32 callers convert) */
   nc_grid grids[4];
   nc_decoder_params dec[4];

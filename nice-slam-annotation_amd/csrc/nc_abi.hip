@@ -3,7 +3,8 @@
 // Plans the launches of one render_batch_ray forward / backward:
 //   forward : [k_depth_max] -> k_ray_setup -> k_mlp_fwd (all decoders of the
 //             stage in one launch) -> k_composite_fwd
-//   backward: k_composite_bwd -> k_mlp_bwd -> [k_param_reduce] -> [k_ray_grads]
+//   backward: k_composite_bwd -> k_mlp_dx -> k_grid_bwd -> [k_mlp_dw -> k_param_reduce]
+//             -> [k_ray_grads]
 // Everything is enqueued on the caller's stream; no host synchronisation, no
 // device allocation (graph-capturable).
 #include <hip/hip_runtime.h>
@@ -33,12 +34,14 @@ int check_hip(int e, const char* what) {
 
 // ---- optional per-kernel event timing (nc_timing_start / nc_timing_stop) ----
 enum KernelId {
-  KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_BWD,
-  KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_COUNT
+  KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
+  KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
+  KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
-                                       "k_composite_bwd", "k_mlp_bwd", "k_param_reduce", "k_ray_grads",
-                                       "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd"};
+                                       "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
+                                       "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
+                                       "k_mlp_dw"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -141,12 +144,14 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, z = 0, pts = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, total = 0;
+  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, rec = 0, drec = 0, total = 0;
+  int64_t rec_off[MAX_JOBS] = {0, 0, 0}, drec_off[MAX_JOBS] = {0, 0, 0};
+  bool save = false;
   int slab_wgs = 1;
   int64_t slab_stride = 0;
 };
 
-void layout(int64_t N, int64_t P, const Plan& pl, bool rays, Ws& w) {
+void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -156,13 +161,27 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, Ws& w) {
   w.dmax = take(16);
   w.z = rays ? take((size_t)P * 8) : 0;
   w.pts = rays ? take((size_t)P * 24) : 0;
+  w.xyz = take((size_t)pl.n_jobs * P * 16);
+  w.pf = take((size_t)P * 16);
   w.occ = take((size_t)pl.n_jobs * P * 4);
   w.rgb = take((size_t)P * 12);
   w.gocc = take((size_t)P * 4);
   w.grgb = take((size_t)P * 12);
   w.dpts = take((size_t)pl.n_jobs * P * 24);
   w.dcbuf = take((size_t)pl.n_jobs * P * 32 * 4);
-  const int64_t blocks = (P + 63) / 64;
+  w.save = save;
+  if (save) {
+    int64_t r = 0, d = 0;
+    for (int j = 0; j < pl.n_jobs; ++j) {
+      w.rec_off[j] = r;
+      w.drec_off[j] = d;
+      r += P * rec_len(pl.jobs[j].kind);
+      d += P * drec_len(pl.jobs[j].kind);
+    }
+    w.rec = take((size_t)r * 4);
+    w.drec = take((size_t)d * 4);
+  }
+  const int64_t blocks = (P + 31) / 32;  // k_mlp_dw sub-chunks
   int per_job = (cu_count() + pl.n_jobs - 1) / pl.n_jobs;
   if (per_job < 1) per_job = 1;
   w.slab_wgs = (int)((blocks < per_job) ? (blocks > 0 ? blocks : 1) : per_job);
@@ -184,8 +203,11 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.n_jobs = pl.n_jobs;
   m.slab_wgs = w.slab_wgs;
   m.slab_stride = w.slab_stride;
+  m.save_rec = w.save;
   for (int j = 0; j < pl.n_jobs; ++j) {
     m.jobs[j] = pl.jobs[j];
+    m.jobs[j].rec_off = w.rec_off[j];
+    m.jobs[j].drec_off = w.drec_off[j];
     const int k = pl.jobs[j].kind;
     m.jobs[j].need_dw = dec[k].grad != nullptr;
     m.jobs[j].need_grid = grids[k].grad != nullptr;
@@ -194,6 +216,8 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   std::memcpy(m.grids, grids, sizeof(m.grids));
   std::memcpy(m.dec, dec, sizeof(m.dec));
   m.pts = pts;
+  m.xyz = at<float4>(ws, w.xyz);
+  m.pf = at<float4>(ws, w.pf);
   m.occ = at<float>(ws, w.occ);
   m.rgb = at<float>(ws, w.rgb);
   m.gocc = at<float>(ws, w.gocc);
@@ -201,6 +225,8 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.dpts = at<double>(ws, w.dpts);
   m.dcbuf = at<float>(ws, w.dcbuf);
   m.slab = at<float>(ws, w.slab);
+  m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
+  m.drec = w.save ? at<float>(ws, w.drec) : nullptr;
 }
 
 int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S) {
@@ -214,7 +240,8 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
   S = a->n_strat + a->n_surf;
   P = a->n_rays * S;
-  layout(a->n_rays, P, pl, true, w);
+  if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
+  layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, w);
   return 0;
 }
 
@@ -239,6 +266,9 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
   std::memcpy(c.t_surf, a->t_surf, sizeof(c.t_surf));
   c.z = at<double>(ws, w.z);
   c.pts = at<double>(ws, w.pts);
+  c.xyz = at<float4>(ws, w.xyz);
+  c.pf = at<float4>(ws, w.pf);
+  for (int j = 0; j < pl.n_jobs; ++j) std::memcpy(c.job_bound[j], a->dec[pl.jobs[j].kind].bound, sizeof(c.job_bound[j]));
   c.occ = at<float>(ws, w.occ);
   c.rgb = at<float>(ws, w.rgb);
   c.depth = a->depth;
@@ -270,6 +300,21 @@ int64_t nparam_of(int kind) {
     case K_COLOR: return Net<K_COLOR>::NPARAM;
   }
   return -1;
+}
+
+int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s);
+
+// decoder backward: dX chains (+ d features, Fourier point gradient) -> trilinear
+// backward -> weight gradients -> slab reduction
+int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s) {
+  if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
+  if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs), s); }), "k_mlp_dx")) return e;
+  if (int e = check_hip(timed(KID_GRID_BWD, s, [&] { return launch_grid_bwd(m, s); }), "k_grid_bwd")) return e;
+  bool any_dw = false;
+  for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;
+  if (any_dw)
+    if (int e = check_hip(timed(KID_MLP_DW, s, [&] { return launch_mlp_dw(m, s); }), "k_mlp_dw")) return e;
+  return reduce_params(m, dec, s);
 }
 
 int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s) {
@@ -391,9 +436,7 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   for (int j = 0; j < m.n_jobs; ++j) any |= m.jobs[j].need_dw || m.jobs[j].need_grid;
   if (!any) return 0;
   if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
-  if (int e = check_hip(timed(KID_MLP_BWD, s, [&] { return launch_mlp_bwd(m, s); }), "k_mlp_bwd")) return e;
-  if (int e = check_hip(timed(KID_GRID_BWD, s, [&] { return launch_grid_bwd(m, s); }), "k_grid_bwd")) return e;
-  if (int e = reduce_params(m, a->dec, s)) return e;
+  if (int e = mlp_backward(m, a->dec, P, s)) return e;
   if (need_coord)
     if (int e = check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(rc, s); }), "k_ray_grads")) return e;
   return 0;
@@ -404,7 +447,8 @@ static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
   if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
   if (int e = plan_stage(a->stage, pl)) return e;
   if (a->n_points < 0) return fail(-1, "nicecore: n_points < 0");
-  layout(0, a->n_points, pl, false, w);
+  if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
+  layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, w);
   return 0;
 }
 
@@ -426,6 +470,7 @@ int nc_points_forward(const nc_points_args* a, void* ws, size_t ws_bytes, void* 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   MlpCtx m;
   fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, false);
+  if (int e = check_hip(launch_points_prep(m, (float4*)m.xyz, (float4*)m.pf, s), "k_points_prep")) return e;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(a->n_points, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
   return check_hip(timed(KID_POINTS_ASSEMBLE, s, [&] { return launch_points_assemble(m, a->stage, a->raw, s); }), "k_points_assemble");
 }
@@ -443,9 +488,7 @@ int nc_points_backward(const nc_points_args* a, void* ws, size_t ws_bytes, void*
   fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, a->g_pts != nullptr);
   if (int e = check_hip(timed(KID_POINTS_SPLIT, s, [&] { return launch_points_split_grad(m, a->stage, a->g_raw, (float*)m.gocc, (float*)m.grgb, s); }), "k_points_split_grad"))
     return e;
-  if (int e = check_hip(timed(KID_MLP_BWD, s, [&] { return launch_mlp_bwd(m, s); }), "k_mlp_bwd")) return e;
-  if (int e = check_hip(timed(KID_GRID_BWD, s, [&] { return launch_grid_bwd(m, s); }), "k_grid_bwd")) return e;
-  if (int e = reduce_params(m, a->dec, s)) return e;
+  if (int e = mlp_backward(m, a->dec, a->n_points, s)) return e;
   if (a->g_pts)
     if (int e = check_hip(timed(KID_POINTS_GRADS, s, [&] { return launch_points_grads(m, a->g_pts, s); }), "k_points_grads")) return e;
   return 0;

@@ -162,6 +162,11 @@ template <bool VEC>
 __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int g, float out[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) out[j] = 0.f;
+#ifdef NC_ABL_NO_GATHER  // timing-only ablation: no global loads
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = c.w[j] * 0.01f;
+  return;
+#endif
   const int64_t sC = G.stride[0];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {

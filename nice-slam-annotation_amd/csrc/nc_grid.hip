@@ -134,11 +134,8 @@ __global__ void __launch_bounds__(256) k_grid_bwd(const MlpCtx ctx) {
   for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
     const int64_t p = t * 16 + i;
     const bool valid = p < ctx.P;
-    double pt[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) pt[k] = valid ? ctx.pts[p * 3 + k] : D.bound[k][0];
-    float xyz[3];
-    normalize_pt(pt, D.bound, xyz);
+    const float4 n = valid ? ctx.xyz[(int64_t)job.slot * ctx.P + p] : float4{-1.f, -1.f, -1.f, 0.f};
+    const float xyz[3] = {n.x, n.y, n.z};
     Corners co;
     make_corners(G, xyz, co);
     float dc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

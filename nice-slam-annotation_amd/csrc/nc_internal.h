@@ -17,6 +17,8 @@ struct Job {
   int32_t need_grid;   // gradient into its own grid (the fine decoder's middle lookup never has one)
   int32_t need_coord;  // gradient into the sample points
   int32_t pad;
+  int64_t rec_off;     // float offset of this job's forward records in MlpCtx::rec
+  int64_t drec_off;    // float offset of its backward records in MlpCtx::drec
 };
 
 constexpr int MAX_JOBS = 3;
@@ -25,17 +27,23 @@ constexpr int MAX_JOBS = 3;
 struct MlpCtx {
   int64_t P;                 // number of points
   int32_t n_jobs;
-  int32_t slab_wgs;          // workgroups per job in the backward launch (= gridDim.x)
+  int32_t slab_wgs;          // workgroups per job in the k_mlp_dw launch (= gridDim.x)
+  int32_t save_rec;          // forward: write the activation records
+  int32_t pad;
   Job jobs[MAX_JOBS];
   nc_grid grids[4];
   nc_decoder_params dec[4];
   const double* pts;         // [P,3] float64 sample points
+  const float4* xyz;         // [n_jobs][P] normalize_3d_coordinate(p, decoder bound).float() (w unused)
+  const float4* pf;          // [P] p.float() (w unused)
   float* occ;                // [n_jobs][P] occupancy outputs (occupancy decoders)
   float* rgb;                // [P][3] colour-decoder outputs (channels 0..2)
   const float* gocc;         // [P] d loss / d occupancy (shared by the occupancy decoders)
   const float* grgb;         // [P][3] d loss / d rgb
   double* dpts;              // [n_jobs][P][3] per-decoder point gradients
-  float* dcbuf;              // [n_jobs][P][32] d loss / d own-grid features (k_mlp_bwd -> k_grid_bwd)
+  float* dcbuf;              // [n_jobs][P][32] d loss / d own-grid features (k_mlp_dx -> k_grid_bwd)
+  float* rec;                // per job [P][Rec::LEN]  forward activations (k_mlp_fwd -> dx, dw)
+  float* drec;               // per job [P][Rec::DLEN] backward activations (k_mlp_dx -> k_mlp_dw)
   float* slab;               // [n_jobs][slab_wgs][slab_stride] per-workgroup parameter gradients
   int64_t slab_stride;
 };
@@ -59,6 +67,9 @@ struct RayCtx {
   double t_surf[NC_MAX_SURF];
   double* z;             // [N][S]
   double* pts;           // [P][3]
+  float4* xyz;           // [n_jobs][P] normalised coordinates per job's decoder bound
+  float4* pf;            // [P] p.float()
+  double job_bound[MAX_JOBS][3][2];
   const float* occ;      // [n_jobs][P]
   const float* rgb;      // [P][3]
   double* depth;
@@ -95,15 +106,20 @@ int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s
 int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, float* gocc, float* grgb,
                              hipStream_t s);
 int launch_points_grads(const MlpCtx& m, double* g_pts, hipStream_t s);
+int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s);
 
 int mlp_fwd_lds_bytes();
-int mlp_bwd_lds_bytes();
+int mlp_dw_lds_bytes();
+int rec_len(int kind);   // floats per point of a decoder's forward record
+int drec_len(int kind);  // ... and of its backward record
 int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);
-int launch_mlp_bwd(const MlpCtx& c, hipStream_t s);
+int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s);
+int launch_mlp_dw(const MlpCtx& c, hipStream_t s);
 int launch_grid_bwd(const MlpCtx& c, hipStream_t s);
 int64_t max_param_count();
 
 constexpr int FWD_THREADS = 512;  // 8 waves, 128 points per workgroup iteration
-constexpr int BWD_THREADS = 256;  // 4 waves, 64 points per workgroup sub-chunk
+constexpr int DX_THREADS = 512;   // 8 waves x 16 points, barrier-free
+constexpr int DW_THREADS = 1024;  // 16 waves own the dW tiles; 32-point sub-chunks
 
 }  // namespace nc

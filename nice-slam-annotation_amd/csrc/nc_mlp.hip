@@ -30,6 +30,9 @@
 #ifdef NC_ABL_FAST_TRIG  // timing-only ablation: hardware sin/cos (wrong for large arguments)
 #define NC_SIN __sinf
 #define NC_COS __cosf
+#elif defined(NC_ABL_NO_TRIG)  // timing-only ablation: no trig at all
+#define NC_SIN(x) (x)
+#define NC_COS(x) (x)
 #else
 #define NC_SIN sinf
 #define NC_COS cosf
@@ -128,7 +131,6 @@ struct WaveRegs {
   float h[5][8];                       // block outputs h_0..h_4 (C layout)
   unsigned mask_lo, mask_hi;           // relu(Z) > 0 bits: layer L reg j -> bit 8L+j (L=4 in hi)
   float pf[3];                         // p.float()
-  double p[3];                         // sample point (float64)
 };
 
 __device__ __forceinline__ bool mask_bit(unsigned lo, unsigned hi, int L, int j) {
@@ -136,15 +138,18 @@ __device__ __forceinline__ bool mask_bit(unsigned lo, unsigned hi, int L, int j)
 }
 
 template <int KIND>
-__device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx, int64_t p, bool valid,
-                                             int i, int g, WaveRegs<KIND>& R, float out[4]) {
+__device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx, int slot, int64_t p,
+                                             bool valid, int i, int g, WaveRegs<KIND>& R, float out[4]) {
   using N = Net<KIND>;
-  const nc_decoder_params& D = ctx.dec[KIND];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) R.p[k] = valid ? ctx.pts[p * 3 + k] : D.bound[k][0];
-  // grid features (decoder.py:179-188 / :196-202)
+  // grid features (decoder.py:179-188 / :196-202); coordinates normalised once per
+  // point by k_ray_setup / k_points_prep
   float xyz[3];
-  normalize_pt(R.p, D.bound, xyz);
+  {
+    const float4 n = valid ? ctx.xyz[(int64_t)slot * ctx.P + p] : float4{-1.f, -1.f, -1.f, 0.f};
+    xyz[0] = n.x; xyz[1] = n.y; xyz[2] = n.z;
+    const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
+    R.pf[0] = f.x; R.pf[1] = f.y; R.pf[2] = f.z;
+  }
   const nc_grid& G = ctx.grids[KIND];
   {
     Corners co;
@@ -162,8 +167,6 @@ __device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx
   // Fourier embedding: sin(p.float() @ B), K=3 summed as fma(p2,B2, fma(p1,B1, p0*B0))
   // which is bit-identical to the CPU reference's sgemm for this shape.
   if constexpr (N::XYZ) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) R.pf[k] = (float)R.p[k];
     const float* B = lds + N::FB;
 #pragma unroll
     for (int j = 0; j < 24; ++j) {
@@ -236,6 +239,43 @@ __device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx
   }
 }
 
+// ---------------------------------------------------------------------------
+// Per-point activation record saved by the forward for the backward kernels
+// (float offsets; every block starts on a 16-byte boundary):
+//   [emb 96 (xyz decoders)] [h_0..h_4 5x32] [c CD] [relu masks: lane-group g -> u32 lo, hi]
+// Backward record written by k_mlp_dx: [dh_0..dh_4 5x32] [dx 96 (xyz)] where dh_L is
+// d loss / d h_L (block L's output) and dx = d loss / d (p @ B).
+// ---------------------------------------------------------------------------
+template <int KIND>
+struct Rec {
+  using N = Net<KIND>;
+  static constexpr int EMB = 0;
+  static constexpr int H = N::XYZ ? EMBP : 0;
+  static constexpr int C = H + 5 * HID;
+  static constexpr int M = C + N::CD;
+  static constexpr int LEN = M + 8;
+  static constexpr int DH = 0;
+  static constexpr int DX = 5 * HID;
+  static constexpr int DLEN = DX + (N::XYZ ? EMBP : 0);
+};
+
+template <int NT>
+__device__ __forceinline__ void store_rows(float* dst, const float* v, int g) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    *reinterpret_cast<float4*>(dst + 16 * t + 4 * g) = float4{v[4 * t + 0], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
+}
+
+template <int KIND>
+__device__ __forceinline__ void save_record(float* r, const WaveRegs<KIND>& R, int g) {
+  using RC = Rec<KIND>;
+  if constexpr (Net<KIND>::XYZ) store_rows<6>(r + RC::EMB, R.emb, g);
+#pragma unroll
+  for (int L = 0; L < 5; ++L) store_rows<2>(r + RC::H + HID * L, R.h[L], g);
+  store_rows<Net<KIND>::CD / 16>(r + RC::C, R.c, g);
+  *reinterpret_cast<uint2*>(r + RC::M + 2 * g) = uint2{R.mask_lo, R.mask_hi};
+}
+
 // Constant-index select: a dynamic index into the by-value kernel-argument block
 // would make the compiler copy the whole block to scratch.
 __device__ __forceinline__ Job pick_job(const Job (&jobs)[MAX_JOBS], unsigned y) {
@@ -260,7 +300,8 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     const bool valid = p < ctx.P;
     WaveRegs<KIND> R;
     float out[4];
-    wave_forward<KIND>(lds, ctx, p, valid, i, g, R, out);
+    wave_forward<KIND>(lds, ctx, job.slot, p, valid, i, g, R, out);
+    if (ctx.save_rec && valid) save_record<KIND>(ctx.rec + job.rec_off + p * Rec<KIND>::LEN, R, g);
     if (valid && g == 0) {
       if constexpr (KIND == K_COLOR) {
         ctx.rgb[p * 3 + 0] = out[0];
@@ -282,51 +323,6 @@ __global__ void __launch_bounds__(FWD_THREADS) k_mlp_fwd(const MlpCtx ctx) {
     case K_FINE: fwd_job<K_FINE>(ctx, job, lds); break;
     default: fwd_job<K_COLOR>(ctx, job, lds); break;
   }
-}
-
-// ---------------------------------------------------------------------------
-// backward: weight-gradient phases
-// ---------------------------------------------------------------------------
-constexpr int CH = 64;  // points per sub-chunk (4 waves x 16)
-
-// dW[16*to + r][16*ti + c] += sum over the 64 staged points of Y[pt][.] X[pt][.]
-// Tiles tau = wave + 4*s (s < NS) of an NR x NC tile grid.  With BIAS, the owner
-// of a first-column tile also adds the row sums of Y (the bias gradient) into the
-// LDS accumulator bacc[16*to + r].
-template <int NR, int NC, int NS, bool BIAS>
-__device__ __forceinline__ void dw_phase(const float* Y, int ldY, const float* X, int ldX, floatx4* acc,
-                                         float* bacc, int wave, int i, int g) {
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int tau = wave + 4 * s;
-    if (tau < NR * NC) {
-      const int to = tau / NC, ti = tau - to * NC;
-      const float* y = Y + g * ldY + 16 * to + i;
-      const float* x = X + g * ldX + 16 * ti + i;
-      floatx4 a = acc[s];
-      float bs = 0.f;
-#pragma unroll
-      for (int q = 0; q < CH / 4; ++q) {
-        const float av = y[4 * q * ldY];
-        a = mfma4(av, x[4 * q * ldX], a);
-        if (BIAS) bs += av;
-      }
-      acc[s] = a;
-      if (BIAS && ti == 0) {
-        bs = sum_groups(bs);
-        if (g == 0) atomicAdd(bacc + 16 * to + i, bs);
-      }
-    }
-  }
-}
-
-// write 16 points x (4*NT) features of this wave (C layout) as rows of an LDS image
-template <int NT>
-__device__ __forceinline__ void stage_rows(float* img, int ld, int col0, const float* v, int row, int g) {
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-    *reinterpret_cast<float4*>(img + row * ld + col0 + 16 * t + 4 * g) =
-        float4{v[4 * t + 0], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
 }
 
 // flat-parameter index of a dW tile element, or -1 (padding)
@@ -355,105 +351,33 @@ struct PhaseMap {
   }
 };
 
-template <int KIND, int NR, int NC, int NS>
-__device__ __forceinline__ void flush_phase(float* img, int ph, const floatx4* acc, int wave, int i, int g) {
-  using PM = PhaseMap<KIND>;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int tau = wave + 4 * s;
-    if (tau < NR * NC) {
-      const int to = tau / NC, ti = tau - to * NC;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t idx = PM::w_index(ph, 16 * to + 4 * g + r, 16 * ti + i);
-        if (idx >= 0) atomicAdd(img + idx, acc[s][r]);
-      }
-    }
-  }
-}
-
-// slot bookkeeping per decoder kind
+// ---------------------------------------------------------------------------
+// k_mlp_dx: backward through the decoder per wavefront (16 points), no barriers.
+// dh_4 = W_out^T d out; per block L (4..0): dz = dh ⊙ relu'(Z_L); d features +=
+// Wc_L^T dh (own 32 channels only); dh_{L-1} / d emb = W_L^T dz (MFMA).  Fourier:
+// dx = d emb ⊙ cos(p @ B); d p.float() = B dx.  Writes dh_L and dx for k_mlp_dw,
+// d features for k_grid_bwd and the Fourier part of the point gradient.
+// ---------------------------------------------------------------------------
 template <int KIND>
-struct Slots {
+__device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float* lds) {
   using N = Net<KIND>;
-  static constexpr int NC0 = N::IN0 / 16, NC3 = N::IN3 / 16, NCC = N::CD / 16;
-  static constexpr int ns(int tiles) { return (tiles + 3) / 4; }
-  static constexpr int OUT = 0;
-  static constexpr int L4 = OUT + ns(2);
-  static constexpr int C4 = L4 + ns(4);
-  static constexpr int L3 = C4 + (N::XYZ ? ns(2 * NCC) : 0);
-  static constexpr int C3 = L3 + ns(2 * NC3);
-  static constexpr int L2 = C3 + (N::XYZ ? ns(2 * NCC) : 0);
-  static constexpr int C2 = L2 + ns(4);
-  static constexpr int L1 = C2 + (N::XYZ ? ns(2 * NCC) : 0);
-  static constexpr int C1 = L1 + ns(4);
-  static constexpr int L0 = C1 + (N::XYZ ? ns(2 * NCC) : 0);
-  static constexpr int C0 = L0 + ns(2 * NC0);
-  static constexpr int FB = C0 + (N::XYZ ? ns(2 * NCC) : 0);
-  static constexpr int TOTAL = FB + (N::XYZ ? ns(6) : 0);
-  __host__ __device__ static constexpr int lin(int L) {
-    return L == 4 ? L4 : L == 3 ? L3 : L == 2 ? L2 : L == 1 ? L1 : L0;
-  }
-  __host__ __device__ static constexpr int fc(int L) {
-    return L == 4 ? C4 : L == 3 ? C3 : L == 2 ? C2 : L == 1 ? C1 : C0;
-  }
-};
-
-// LDS carve-up of the backward kernel (floats)
-template <int KIND>
-struct BwdLds {
-  using N = Net<KIND>;
-  static constexpr int LDCB = N::CD + 16;  // c image leading dim (== 16 mod 32)
-  static constexpr int CBUF = N::WEIGHTS;
-  static constexpr int STAGE = CBUF + (N::XYZ ? CH * LDCB : 0);
-  static constexpr int STAGE_FLOATS = CH * (48 + 144);
-  static constexpr int BACC = STAGE + STAGE_FLOATS;  // bias-gradient accumulators
-  // per phase id (see PhaseMap): 0 out (16), 1..5 pts_linears[4..0] (32 each), 6..10 fc_c[4..0]
-  __host__ __device__ static constexpr int bacc_off(int ph) { return ph == 0 ? 0 : 16 + 32 * (ph - 1); }
-  static constexpr int BACC_FLOATS = 16 + 32 * 10;
-  static constexpr int TOTAL = BACC + BACC_FLOATS;
-};
-
-__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int BWD_LDS_FLOATS =
-    cmax(cmax(BwdLds<K_COARSE>::TOTAL, BwdLds<K_MID>::TOTAL), cmax(BwdLds<K_FINE>::TOTAL, BwdLds<K_COLOR>::TOTAL));
-constexpr int FWD_LDS_FLOATS =
-    cmax(cmax(Net<K_COARSE>::WEIGHTS, Net<K_MID>::WEIGHTS), cmax(Net<K_FINE>::WEIGHTS, Net<K_COLOR>::WEIGHTS));
-static_assert(BWD_LDS_FLOATS * 4 <= 160 * 1024, "backward LDS budget");
-
-template <int KIND>
-__device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float* lds) {
-  using N = Net<KIND>;
-  using SL = Slots<KIND>;
-  using BL = BwdLds<KIND>;
+  using RC = Rec<KIND>;
   load_weights<KIND>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int row = wave * 16 + i;
-  float* cbuf = lds + BL::CBUF;
-  float* stg = lds + BL::STAGE;
+  const int waves = blockDim.x >> 6;
   const bool need_dw = job.need_dw != 0;
-  const bool need_grid = job.need_grid != 0 && ctx.grids[KIND].grad != nullptr;
+  const bool need_grid = job.need_grid != 0;
   const bool need_coord = job.need_coord != 0;
   const bool need_dc = need_grid || need_coord;
-
-  floatx4 acc[SL::TOTAL];
-#pragma unroll
-  for (int s = 0; s < SL::TOTAL; ++s) acc[s] = zero4();
-  float* bacc = lds + BL::BACC;
-  for (int e = threadIdx.x; e < BL::BACC_FLOATS; e += blockDim.x) bacc[e] = 0.f;
-  __syncthreads();
-
-  const int64_t nblk = (ctx.P + CH - 1) / CH;
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    asm volatile("" ::: "memory");  // no hoisting of LDS weight reads (see fwd_job)
-    const int64_t p = blk * CH + row;
+  const int64_t ntiles = (ctx.P + 15) / 16;
+  for (int64_t t = (int64_t)blockIdx.x * waves + wave; t < ntiles; t += (int64_t)gridDim.x * waves) {
+    asm volatile("" ::: "memory");  // keep LDS weight reads inside the loop (see fwd_job)
+    const int64_t p = t * 16 + i;
     const bool valid = p < ctx.P;
-    WaveRegs<KIND> R;
-    float out[4];
-    wave_forward<KIND>(lds, ctx, p, valid, i, g, R, out);
-
-    // upstream gradient of this decoder's output (decoder.py:345-370 stage wiring)
+    const float* rec = ctx.rec + job.rec_off + (valid ? p : 0) * RC::LEN;
+    float* drec = ctx.drec + job.drec_off + (valid ? p : 0) * RC::DLEN;
     float dout[4] = {0.f, 0.f, 0.f, 0.f};
+    unsigned mlo = 0, mhi = 0;
     if (valid) {
       if constexpr (KIND == K_COLOR) {
         dout[0] = ctx.grgb[p * 3 + 0];
@@ -462,6 +386,9 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
       } else {
         dout[0] = ctx.gocc[p];
       }
+      const uint2 m = *reinterpret_cast<const uint2*>(rec + RC::M + 2 * g);
+      mlo = m.x;
+      mhi = m.y;
     }
     float dh[8];
 #pragma unroll
@@ -471,91 +398,34 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
       for (int o = 0; o < N::NOUT; ++o) s = s + lds[N::WO + o * HID + feat_of(j, g)] * dout[o];
       dh[j] = s;
     }
-    if (need_dw) {
-      float* Y = stg;
-      float* X = stg + CH * 16;
-      *reinterpret_cast<float4*>(Y + row * 16 + 4 * g) =
-          g == 0 ? float4{dout[0], dout[1], dout[2], dout[3]} : float4{0.f, 0.f, 0.f, 0.f};
-      stage_rows<2>(X, 48, 0, R.h[4], row, g);
-      if constexpr (N::XYZ) stage_rows<N::CD / 16>(cbuf, BL::LDCB, 0, R.c, row, g);
-      __syncthreads();
-      dw_phase<1, 2, 1, true>(Y, 16, X, 48, acc + SL::OUT, bacc + BL::bacc_off(0), wave, i, g);
-      __syncthreads();
-    }
-
     floatx4 dc[2] = {zero4(), zero4()};
     floatx4 demb[6] = {zero4(), zero4(), zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
     for (int L = 4; L >= 0; --L) {
+      if (need_dw && valid) store_rows<2>(drec + RC::DH + HID * L, dh, g);
       float dz[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dz[j] = mask_bit(R.mask_lo, R.mask_hi, L, j) ? dh[j] : 0.f;
-      // dF (fc_c branch) -> d features (only the decoder's own 32 channels carry grad)
+      for (int j = 0; j < 8; ++j) dz[j] = mask_bit(mlo, mhi, L, j) ? dh[j] : 0.f;
       if constexpr (N::XYZ) {
         if (need_dc) mm_bwd<2, N::LDC>(lds + N::WC + L * HID * N::LDC, 0, dh, dc, i, g);
       }
-      // weight-gradient phases for this block (before dh is overwritten)
-      if (need_dw) {
-        float* Y = stg;
-        float* X = stg + CH * 48;
-        stage_rows<2>(Y, 48, 0, dz, row, g);
-        int ldx;
-        if (L == 0) {
-          if constexpr (N::XYZ) { ldx = 112; stage_rows<6>(X, ldx, 0, R.emb, row, g); }
-          else { ldx = 48; stage_rows<2>(X, ldx, 0, R.c, row, g); }
-        } else if (L == 3) {
-          if constexpr (N::XYZ) {
-            ldx = 144;
-            stage_rows<6>(X, ldx, 0, R.emb, row, g);
-            stage_rows<2>(X, ldx, 96, R.h[2], row, g);
-          } else {
-            ldx = 80;
-            stage_rows<2>(X, ldx, 0, R.c, row, g);
-            stage_rows<2>(X, ldx, 32, R.h[2], row, g);
-          }
-        } else {
-          ldx = 48;
-          stage_rows<2>(X, ldx, 0, R.h[L > 0 ? L - 1 : 0], row, g);
-        }
-        __syncthreads();
-        if (L == 0) {
-          dw_phase<2, SL::NC0, SL::ns(2 * SL::NC0), true>(Y, 48, X, ldx, acc + SL::L0, bacc + BL::bacc_off(5 - L), wave, i, g);
-        } else if (L == 3) {
-          dw_phase<2, SL::NC3, SL::ns(2 * SL::NC3), true>(Y, 48, X, ldx, acc + SL::L3, bacc + BL::bacc_off(5 - L), wave, i, g);
-        } else {
-          dw_phase<2, 2, 1, true>(Y, 48, X, ldx, acc + SL::lin(L), bacc + BL::bacc_off(5 - L), wave, i, g);
-        }
-        __syncthreads();
-        if constexpr (N::XYZ) {
-          stage_rows<2>(Y, 48, 0, dh, row, g);
-          __syncthreads();
-          dw_phase<2, SL::NCC, SL::ns(2 * SL::NCC), true>(Y, 48, cbuf, BL::LDCB, acc + SL::fc(L),
-                                                          bacc + BL::bacc_off(10 - L), wave, i, g);
-          __syncthreads();
-        }
-      }
-      // dX = W_L^T dZ
       const float* W = lds + N::lin_off(L);
       if (L == 0) {
         if constexpr (N::XYZ) mm_bwd<6, N::LD0>(W, 0, dz, demb, i, g);
         else if (need_dc) mm_bwd<2, N::LD0>(W, 0, dz, dc, i, g);
-      } else if (L == 3) {
-        floatx4 t2[2] = {zero4(), zero4()};
-        if constexpr (N::XYZ) {
-          mm_bwd<6, N::LD3>(W, 0, dz, demb, i, g);
-          mm_bwd<2, N::LD3>(W, 6, dz, t2, i, g);
-        } else {
-          if (need_dc) mm_bwd<2, N::LD3>(W, 0, dz, dc, i, g);
-          mm_bwd<2, N::LD3>(W, 2, dz, t2, i, g);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dh[r] = t2[0][r];
-          dh[4 + r] = t2[1][r];
-        }
       } else {
         floatx4 t2[2] = {zero4(), zero4()};
-        mm_bwd<2, N::LDH>(W, 0, dz, t2, i, g);
+        if (L == 3) {
+          if constexpr (N::XYZ) {
+            mm_bwd<6, N::LD3>(W, 0, dz, demb, i, g);
+            mm_bwd<2, N::LD3>(W, 6, dz, t2, i, g);
+          } else {
+            if (need_dc) mm_bwd<2, N::LD3>(W, 0, dz, dc, i, g);
+            mm_bwd<2, N::LD3>(W, 2, dz, t2, i, g);
+          }
+        } else {
+          mm_bwd<2, N::LDH>(W, 0, dz, t2, i, g);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           dh[r] = t2[0][r];
@@ -563,19 +433,18 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
         }
       }
     }
-
-    // Fourier chain: d emb -> d x (cos), -> d p.float() and d B
     float dpf[3] = {0.f, 0.f, 0.f};
     if constexpr (N::XYZ) {
       const float* B = lds + N::FB;
+      const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
       float dx[24];
 #pragma unroll
       for (int j = 0; j < 24; ++j) {
         const int m = feat_of(j, g);
-        const float x = __builtin_fmaf(R.pf[2], B[2 * EMBP + m],
-                                       __builtin_fmaf(R.pf[1], B[EMBP + m], R.pf[0] * B[m]));
+        const float x = __builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m]));
         dx[j] = (m < EMB) ? demb[j >> 2][j & 3] * NC_COS(x) : 0.f;
       }
+      if (need_dw && valid) store_rows<6>(drec + RC::DX, dx, g);
       if (need_coord) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -585,20 +454,7 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
           dpf[k] = sum_groups(s);
         }
       }
-      if (need_dw) {
-        float* Y = stg;
-        float* X = stg + CH * 112;
-        stage_rows<6>(Y, 112, 0, dx, row, g);
-        *reinterpret_cast<float4*>(X + row * 16 + 4 * g) =
-            g == 0 ? float4{R.pf[0], R.pf[1], R.pf[2], 0.f} : float4{0.f, 0.f, 0.f, 0.f};
-        __syncthreads();
-        dw_phase<6, 1, 2, false>(Y, 112, X, 16, acc + SL::FB, nullptr, wave, i, g);
-        __syncthreads();
-      }
     }
-
-    // hand the trilinear backward to k_grid_bwd: d features (this decoder's own 32
-    // channels, C layout) and the Fourier part of the point gradient
     if (need_dc && valid) {
       float* dst = ctx.dcbuf + ((int64_t)job.slot * ctx.P + p) * HID;
       *reinterpret_cast<float4*>(dst + 4 * g) = float4{dc[0][0], dc[0][1], dc[0][2], dc[0][3]};
@@ -610,81 +466,313 @@ __device__ __forceinline__ void bwd_job(const MlpCtx& ctx, const Job& job, float
       for (int k = 0; k < 3; ++k) dst[k] = (double)dpf[k];
     }
   }
-
-  if (!need_dw) return;
-  // flush register-resident dW tiles -> LDS image of the flat parameter vector -> slab
-  __syncthreads();
-  float* img = lds;
-  for (int e = threadIdx.x; e < N::NPARAM; e += blockDim.x) img[e] = 0.f;
-  __syncthreads();
-  flush_phase<KIND, 1, 2, 1>(img, 0, acc + SL::OUT, wave, i, g);
-#pragma unroll
-  for (int L = 4; L >= 0; --L) {
-    if (L == 0) flush_phase<KIND, 2, SL::NC0, SL::ns(2 * SL::NC0)>(img, 5 - L, acc + SL::L0, wave, i, g);
-    else if (L == 3) flush_phase<KIND, 2, SL::NC3, SL::ns(2 * SL::NC3)>(img, 5 - L, acc + SL::L3, wave, i, g);
-    else flush_phase<KIND, 2, 2, 1>(img, 5 - L, acc + SL::lin(L), wave, i, g);
-    if constexpr (N::XYZ)
-      flush_phase<KIND, 2, SL::NCC, SL::ns(2 * SL::NCC)>(img, 10 - L, acc + SL::fc(L), wave, i, g);
-  }
-  if constexpr (N::XYZ) flush_phase<KIND, 6, 1, 2>(img, 11, acc + SL::FB, wave, i, g);
-  // bias gradients from the LDS accumulators
-  for (int e = threadIdx.x; e < BL::BACC_FLOATS; e += blockDim.x) {
-    int ph, row;
-    if (e < 16) { ph = 0; row = e; }
-    else { ph = 1 + (e - 16) / 32; row = (e - 16) % 32; }
-    if (ph > 5 && !N::XYZ) continue;
-    const int64_t bi = PhaseMap<KIND>::b_index(ph, row);
-    if (bi >= 0) img[bi] += bacc[e];
-  }
-  __syncthreads();
-  float* slab = ctx.slab + ((int64_t)blockIdx.y * ctx.slab_wgs + blockIdx.x) * ctx.slab_stride;
-  for (int e = threadIdx.x; e < N::NPARAM; e += blockDim.x) slab[e] = img[e];
 }
 
-__global__ void __launch_bounds__(BWD_THREADS) k_mlp_bwd(const MlpCtx ctx) {
+__global__ void __launch_bounds__(DX_THREADS) k_mlp_dx(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Job job = pick_job(ctx.jobs, blockIdx.y);
+  if (!job.need_dw && !job.need_grid && !job.need_coord) return;
   switch (job.kind) {
-    case K_COARSE: bwd_job<K_COARSE>(ctx, job, lds); break;
-    case K_MID: bwd_job<K_MID>(ctx, job, lds); break;
-    case K_FINE: bwd_job<K_FINE>(ctx, job, lds); break;
-    default: bwd_job<K_COLOR>(ctx, job, lds); break;
+    case K_COARSE: dx_job<K_COARSE>(ctx, job, lds); break;
+    case K_MID: dx_job<K_MID>(ctx, job, lds); break;
+    case K_FINE: dx_job<K_FINE>(ctx, job, lds); break;
+    default: dx_job<K_COLOR>(ctx, job, lds); break;
   }
 }
 
 // ---------------------------------------------------------------------------
-// launch wrappers
+// k_mlp_dw: weight gradients dW = sum_points dY^T X as a streamed GEMM.
+// Each workgroup walks 32-point sub-chunks of one decoder: the points' forward
+// and backward records are copied contiguously into LDS ([point][record] rows,
+// row length == 16 mod 32 floats -> conflict-free ds_read_b32 operands), then
+// every dW tile of every layer (16x16, table DwTiles) is advanced by 8 MFMA
+// k-steps of 4 points.  Tiles are owned by waves for the whole kernel and kept in
+// registers; bias gradients (row sums of dY) go to LDS float atomics.  One flush
+// per workgroup into a slab, summed by k_param_reduce.
 // ---------------------------------------------------------------------------
+constexpr int DW_NPTS = 32;
+
+template <int KIND>
+struct DwLayout {
+  using RC = Rec<KIND>;
+  static constexpr int DREC = RC::LEN;           // backward record follows the forward one
+  static constexpr int PF = DREC + RC::DLEN;     // p.float() (4)
+  static constexpr int DOUT = PF + 4;            // d out (4; rows >= NOUT zero)
+  static constexpr int RS = DOUT + 4;            // row stride (== 16 mod 32)
+  static constexpr int BUF = DW_NPTS * RS;
+  static constexpr int BACC = BUF;               // bias accumulators after the buffer
+  static constexpr int BACC_FLOATS = 16 + 32 * 10;
+  static constexpr int TOTAL = BACC + BACC_FLOATS;
+  static_assert(RS % 32 == 16, "row stride must be 16 mod 32 for conflict-free operand reads");
+};
+
+// dW tile list of a decoder: phase ids as PhaseMap (0 out, 1..5 lin L=5-ph, 6..10 fc
+// L=10-ph, 11 Fourier B); (to, ti) = 16-row block of dY, 16-column block of X.
+template <int KIND>
+struct DwTiles {
+  using N = Net<KIND>;
+  static constexpr int NC0 = N::IN0 / 16, NC3 = N::IN3 / 16, NCC = N::CD / 16;
+  __host__ __device__ static constexpr int ncols(int ph) {
+    return ph == 0 ? 2 : ph == 1 ? 2 : ph == 2 ? NC3 : ph == 3 ? 2 : ph == 4 ? 2 : ph == 5 ? NC0 : ph <= 10 ? NCC : 1;
+  }
+  __host__ __device__ static constexpr int nrows(int ph) { return ph == 0 ? 1 : ph <= 10 ? 2 : 6; }
+  __host__ __device__ static constexpr bool present(int ph) { return N::XYZ || ph <= 5; }
+  __host__ __device__ static constexpr int count() {
+    int n = 0;
+    for (int ph = 0; ph < 12; ++ph)
+      if (present(ph)) n += nrows(ph) * ncols(ph);
+    return n;
+  }
+  static constexpr int NT = count();
+  // packed (ph | to << 8 | ti << 16) of tile tau (branch-free selects, no stack)
+  __device__ __forceinline__ static int code(int tau) {
+    int res = 0, base = 0;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      if (!present(q)) continue;
+      const int n = nrows(q) * ncols(q);
+      const int t = tau - base;
+      res = (t >= 0 && t < n) ? (q | ((t / ncols(q)) << 8) | ((t % ncols(q)) << 16)) : res;
+      base += n;
+    }
+    return res;
+  }
+  __device__ __forceinline__ static void get(int tau, int& ph, int& to, int& ti) {
+    const int c = code(tau);
+    ph = c & 255;
+    to = (c >> 8) & 255;
+    ti = c >> 16;
+  }
+};
+
+constexpr int DW_WAVES = DW_THREADS / 64;
+
+template <int KIND>
+__device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float* lds) {
+  using N = Net<KIND>;
+  using RC = Rec<KIND>;
+  using LY = DwLayout<KIND>;
+  using TL = DwTiles<KIND>;
+  constexpr int NS = (TL::NT + DW_WAVES - 1) / DW_WAVES;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  float* buf = lds;
+  float* bacc = lds + LY::BACC;
+  for (int e = threadIdx.x; e < LY::BACC_FLOATS; e += blockDim.x) bacc[e] = 0.f;
+  floatx4 acc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) acc[s] = zero4();
+  // Per-tile operand descriptors.  The k-step is branch-free: a dY column that does
+  // not exist (output rows >= NOUT) and the Fourier tile's x columns >= 3 read the
+  // always-zero DOUT+3 slot, and tiles without a relu mask test bit 0 of the
+  // all-ones PF+3 slot.
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  unsigned dyx[NS], dm[NS];  // yoff | xoff << 16,  mword | (1 << mbit) bit position << 16
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int tau = wv + DW_WAVES * s;
+    int ph, to, ti;
+    TL::get(tau < TL::NT ? tau : 0, ph, to, ti);
+    const int o = 16 * to + i;
+    int yoff, xoff, mword = LY::PF + 3, mbit = 0;
+    if (ph == 0) {
+      yoff = LY::DOUT + (o < N::NOUT ? o : 3);
+      xoff = RC::H + HID * 4 + 16 * ti + i;
+    } else if (ph <= 5) {
+      const int L = 5 - ph;
+      yoff = LY::DREC + RC::DH + HID * L + o;
+      mword = RC::M + 2 * ((o >> 2) & 3) + (L == 4 ? 1 : 0);
+      mbit = (L == 4 ? 0 : 8 * L) + 4 * (o >> 4) + (o & 3);
+      const int c = 16 * ti + i;
+      if (L == 0) xoff = N::XYZ ? RC::EMB + c : RC::C + c;
+      else if (L == 3) xoff = N::XYZ ? (c < EMBP ? RC::EMB + c : RC::H + HID * 2 + (c - EMBP))
+                                     : (c < HID ? RC::C + c : RC::H + HID * 2 + (c - HID));
+      else xoff = RC::H + HID * (L - 1) + c;
+    } else if (ph <= 10) {
+      yoff = LY::DREC + RC::DH + HID * (10 - ph) + o;
+      xoff = RC::C + 16 * ti + i;
+    } else {
+      yoff = LY::DREC + RC::DX + o;
+      xoff = i < 3 ? LY::PF + i : LY::DOUT + 3;
+    }
+    dyx[s] = (unsigned)yoff | ((unsigned)xoff << 16);
+    dm[s] = (unsigned)mword | ((unsigned)mbit << 16);
+  }
+  // ---- staging: the records of the next sub-chunk are prefetched into registers
+  // (branch-free, PER float4 per thread) while the current one is consumed ----
+  constexpr int R4 = RC::LEN / 4, D4 = RC::DLEN / 4, W4 = R4 + D4;
+  constexpr int ITEMS = DW_NPTS * W4;
+  constexpr int PER = (ITEMS + DW_THREADS - 1) / DW_THREADS;
+  const int64_t nsub = (ctx.P + DW_NPTS - 1) / DW_NPTS;
+  float4 pre[PER];
+  auto prefetch = [&](int64_t sub) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = threadIdx.x + k * DW_THREADS;
+      const int ee = e < ITEMS ? e : ITEMS - 1;
+      const int r = ee / W4, c = ee - r * W4;
+      int64_t p = sub * DW_NPTS + r;
+      p = p < ctx.P ? p : ctx.P - 1;
+      const float* src = c < R4 ? ctx.rec + job.rec_off + p * RC::LEN + 4 * c
+                                : ctx.drec + job.drec_off + p * RC::DLEN + 4 * (c - R4);
+      pre[k] = *reinterpret_cast<const float4*>(src);
+    }
+  };
+  if (blockIdx.x < nsub) prefetch(blockIdx.x);
+  for (int64_t sub = blockIdx.x; sub < nsub; sub += gridDim.x) {
+    __syncthreads();  // previous sub-chunk's reads are done
+    const int64_t p0 = sub * DW_NPTS;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = threadIdx.x + k * DW_THREADS;
+      if (e < ITEMS) {
+        const int r = e / W4, c = e - r * W4;
+        const float4 v = (p0 + r < ctx.P) ? pre[k] : float4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<float4*>(buf + r * LY::RS + 4 * c) = v;
+      }
+    }
+    if (threadIdx.x < 2 * DW_NPTS) {  // p.float() and d out columns
+      const int r = threadIdx.x >> 1;
+      const int64_t p = p0 + r;
+      float4 v = float4{0.f, 0.f, 0.f, 0.f};
+      if (threadIdx.x & 1) {
+        if (p < ctx.P) {
+          if constexpr (KIND == K_COLOR) v = float4{ctx.grgb[p * 3 + 0], ctx.grgb[p * 3 + 1], ctx.grgb[p * 3 + 2], 0.f};
+          else v.x = ctx.gocc[p];
+        }
+        *reinterpret_cast<float4*>(buf + r * LY::RS + LY::DOUT) = v;
+      } else {
+        if (p < ctx.P) v = ctx.pf[p];
+        v.w = __uint_as_float(0xffffffffu);  // all-ones mask slot
+        *reinterpret_cast<float4*>(buf + r * LY::RS + LY::PF) = v;
+      }
+    }
+    __syncthreads();
+    if (sub + gridDim.x < nsub) prefetch(sub + gridDim.x);
+    // ---- tiles: 8 MFMA k-steps of 4 points each ----
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int tau = wv + DW_WAVES * s;
+      if (tau >= TL::NT) continue;  // wave-uniform (scalar) branch
+      floatx4 a = acc[s];
+      float bs = 0.f;
+      // opaque copies: keeps LICM from hoisting 3 x 8 LDS addresses per tile out of
+      // the sub-chunk loop (which spills)
+      unsigned dyx_s = dyx[s], dm_s = dm[s];
+      asm volatile("" : "+v"(dyx_s), "+v"(dm_s));
+      const float* yrow = buf + g * LY::RS + (dyx_s & 0xffffu);
+      const float* xrow = buf + g * LY::RS + (dyx_s >> 16);
+      const float* mrow = buf + g * LY::RS + (dm_s & 0xffffu);
+      const unsigned mbit = 1u << (dm_s >> 16);
+#pragma unroll
+      for (int q = 0; q < DW_NPTS / 4; ++q) {
+        const float y = yrow[4 * q * LY::RS];
+        const float av = (__float_as_uint(mrow[4 * q * LY::RS]) & mbit) ? y : 0.f;
+        a = mfma4(av, xrow[4 * q * LY::RS], a);
+        bs += av;
+      }
+      acc[s] = a;
+      int ph, to, ti;
+      TL::get(tau, ph, to, ti);
+      if (ti == 0 && ph <= 10) {  // wave-uniform
+        bs = sum_groups(bs);
+        if (g == 0) atomicAdd(bacc + (ph == 0 ? 0 : 16 + 32 * (ph - 1)) + 16 * to + i, bs);
+      }
+    }
+  }
+  // ---- flush: every weight-gradient element is owned by exactly one lane and
+  // every bias by one bacc entry, so the slab row is written without an image ----
+  float* slab = ctx.slab + ((int64_t)blockIdx.y * ctx.slab_wgs + blockIdx.x) * ctx.slab_stride;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int tau = wv + DW_WAVES * s;
+    if (tau >= TL::NT) continue;
+    int ph, to, ti;
+    TL::get(tau, ph, to, ti);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t idx = PhaseMap<KIND>::w_index(ph, 16 * to + 4 * g + r, 16 * ti + i);
+      if (idx >= 0) slab[idx] = acc[s][r];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < LY::BACC_FLOATS; e += blockDim.x) {
+    const int ph = e < 16 ? 0 : 1 + (e - 16) / 32;
+    const int row = e < 16 ? e : (e - 16) % 32;
+    if (ph > 5 && !N::XYZ) continue;
+    const int64_t bi = PhaseMap<KIND>::b_index(ph, row);
+    if (bi >= 0) slab[bi] = bacc[e];
+  }
+}
+
+__global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Job job = pick_job(ctx.jobs, blockIdx.y);
+  if (!job.need_dw) return;
+  switch (job.kind) {
+    case K_COARSE: dw_job<K_COARSE>(ctx, job, lds); break;
+    case K_MID: dw_job<K_MID>(ctx, job, lds); break;
+    case K_FINE: dw_job<K_FINE>(ctx, job, lds); break;
+    default: dw_job<K_COLOR>(ctx, job, lds); break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers / layout queries
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int FWD_LDS_FLOATS =
+    cmax(cmax(Net<K_COARSE>::WEIGHTS, Net<K_MID>::WEIGHTS), cmax(Net<K_FINE>::WEIGHTS, Net<K_COLOR>::WEIGHTS));
+constexpr int DW_LDS_FLOATS = cmax(cmax(DwLayout<K_COARSE>::TOTAL, DwLayout<K_MID>::TOTAL),
+                                   cmax(DwLayout<K_FINE>::TOTAL, DwLayout<K_COLOR>::TOTAL));
+static_assert(FWD_LDS_FLOATS * 4 <= 160 * 1024, "weight image LDS budget");
+static_assert(DW_LDS_FLOATS * 4 <= 160 * 1024, "dW staging LDS budget");
+
 int mlp_fwd_lds_bytes() { return FWD_LDS_FLOATS * 4; }
-int mlp_bwd_lds_bytes() { return BWD_LDS_FLOATS * 4; }
+int mlp_dw_lds_bytes() { return DW_LDS_FLOATS * 4; }
 int64_t max_param_count() {
   return cmax(cmax((int)Net<K_COARSE>::NPARAM, (int)Net<K_MID>::NPARAM),
               cmax((int)Net<K_FINE>::NPARAM, (int)Net<K_COLOR>::NPARAM));
 }
+int rec_len(int kind) {
+  switch (kind) {
+    case K_COARSE: return Rec<K_COARSE>::LEN;
+    case K_MID: return Rec<K_MID>::LEN;
+    case K_FINE: return Rec<K_FINE>::LEN;
+    default: return Rec<K_COLOR>::LEN;
+  }
+}
+int drec_len(int kind) {
+  switch (kind) {
+    case K_COARSE: return Rec<K_COARSE>::DLEN;
+    case K_MID: return Rec<K_MID>::DLEN;
+    case K_FINE: return Rec<K_FINE>::DLEN;
+    default: return Rec<K_COLOR>::DLEN;
+  }
+}
+
+template <typename K>
+static int set_lds(K kernel, int bytes) {
+  return (int)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 
 int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_mlp_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       mlp_fwd_lds_bytes());
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
-  dim3 grid(grid_x, c.n_jobs);
-  hipLaunchKernelGGL(k_mlp_fwd, grid, dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
+  static int attr = -1;
+  if (attr != 0 && (attr = set_lds(k_mlp_fwd, mlp_fwd_lds_bytes())) != 0) return attr;
+  hipLaunchKernelGGL(k_mlp_fwd, dim3(grid_x, c.n_jobs), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 
-int launch_mlp_bwd(const MlpCtx& c, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_mlp_bwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       mlp_bwd_lds_bytes());
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
-  dim3 grid(c.slab_wgs, c.n_jobs);
-  hipLaunchKernelGGL(k_mlp_bwd, grid, dim3(BWD_THREADS), mlp_bwd_lds_bytes(), s, c);
+int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s) {
+  static int attr = -1;
+  if (attr != 0 && (attr = set_lds(k_mlp_dx, mlp_fwd_lds_bytes())) != 0) return attr;
+  hipLaunchKernelGGL(k_mlp_dx, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_fwd_lds_bytes(), s, c);
+  return (int)hipGetLastError();
+}
+
+int launch_mlp_dw(const MlpCtx& c, hipStream_t s) {
+  static int attr = -1;
+  if (attr != 0 && (attr = set_lds(k_mlp_dw, mlp_dw_lds_bytes())) != 0) return attr;
+  hipLaunchKernelGGL(k_mlp_dw, dim3(c.slab_wgs, c.n_jobs), dim3(DW_THREADS), mlp_dw_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 

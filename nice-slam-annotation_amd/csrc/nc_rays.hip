@@ -112,8 +112,35 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   if (lane < c.S) {
     const int64_t p = r * c.S + lane;
     c.z[p] = z;
+    double pt[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) c.pts[p * 3 + k] = o[k] + d[k] * z;  // Renderer.py:227-228
+    for (int k = 0; k < 3; ++k) {
+      pt[k] = o[k] + d[k] * z;  // Renderer.py:227-228
+      c.pts[p * 3 + k] = pt[k];
+    }
+    c.pf[p] = float4{(float)pt[0], (float)pt[1], (float)pt[2], 0.f};
+    for (int j = 0; j < c.n_jobs; ++j) {
+      float n[3];
+      normalize_pt(pt, j == 0 ? c.job_bound[0] : (j == 1 ? c.job_bound[1] : c.job_bound[2]), n);
+      c.xyz[(int64_t)j * c.P + p] = float4{n[0], n[1], n[2], 0.f};
+    }
+  }
+}
+
+// points mode (NICE.forward on caller points): the same per-point prologue
+__global__ void k_points_prep(const MlpCtx m, float4* xyz, float4* pf) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m.P) return;
+  double pt[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pt[k] = m.pts[p * 3 + k];
+  pf[p] = float4{(float)pt[0], (float)pt[1], (float)pt[2], 0.f};
+  for (int j = 0; j < m.n_jobs; ++j) {
+    const Job job = j == 0 ? m.jobs[0] : (j == 1 ? m.jobs[1] : m.jobs[2]);
+    const nc_decoder_params& D = job.kind == 0 ? m.dec[0] : job.kind == 1 ? m.dec[1] : job.kind == 2 ? m.dec[2] : m.dec[3];
+    float n[3];
+    normalize_pt(pt, D.bound, n);
+    xyz[(int64_t)j * m.P + p] = float4{n[0], n[1], n[2], 0.f};
   }
 }
 
@@ -357,6 +384,10 @@ int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, flo
                              hipStream_t s) {
   hipLaunchKernelGGL(k_points_split_grad, dim3((unsigned)((m.P + 255) / 256)), dim3(256), 0, s, m, stage,
                      g_raw, gocc, grgb);
+  return (int)hipGetLastError();
+}
+int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s) {
+  hipLaunchKernelGGL(k_points_prep, dim3((unsigned)((m.P + 255) / 256)), dim3(256), 0, s, m, xyz, pf);
   return (int)hipGetLastError();
 }
 int launch_points_grads(const MlpCtx& m, double* g_pts, hipStream_t s) {

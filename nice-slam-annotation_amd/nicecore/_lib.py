@@ -12,7 +12,8 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 1
+NC_ABI_VERSION = 2
+NC_SAVE_FOR_BACKWARD = 1
 NC_MAX_SAMPLES = 64
 NC_MAX_SURF = 32
 
@@ -40,7 +41,7 @@ class NcDecoderParams(ctypes.Structure):
 
 class NcRenderArgs(ctypes.Structure):
     _fields_ = [("abi_version", c_int32), ("stage", c_int32), ("n_rays", c_int64),
-                ("n_strat", c_int32), ("n_surf", c_int32),
+                ("n_strat", c_int32), ("n_surf", c_int32), ("flags", c_int32), ("reserved", c_int32),
                 ("rays_o", c_void_p), ("rays_d", c_void_p), ("gt_depth", c_void_p),
                 ("depth_max", c_void_p), ("bound", (c_double * 2) * 3),
                 ("t_strat", c_float * NC_MAX_SAMPLES), ("t_surf", c_double * NC_MAX_SURF),
@@ -52,7 +53,7 @@ class NcRenderArgs(ctypes.Structure):
 
 class NcPointsArgs(ctypes.Structure):
     _fields_ = [("abi_version", c_int32), ("stage", c_int32), ("n_points", c_int64),
-                ("pts", c_void_p), ("grids", NcGrid * 4), ("dec", NcDecoderParams * 4),
+                ("flags", c_int32), ("reserved", c_int32), ("pts", c_void_p), ("grids", NcGrid * 4), ("dec", NcDecoderParams * 4),
                 ("raw", c_void_p), ("g_raw", c_void_p), ("g_pts", c_void_p)]
 
 
@@ -107,9 +108,9 @@ def check(rc: int, what: str):
 
 
 KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_fwd": 3,
-              "k_composite_bwd": 4, "k_mlp_bwd": 5, "k_param_reduce": 6, "k_ray_grads": 7,
+              "k_composite_bwd": 4, "k_mlp_dx": 5, "k_param_reduce": 6, "k_ray_grads": 7,
               "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10,
-              "k_grid_bwd": 11}
+              "k_grid_bwd": 11, "k_mlp_dw": 12}
 
 
 class KernelTimer:

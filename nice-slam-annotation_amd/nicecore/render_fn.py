@@ -24,22 +24,23 @@ def _ptr(t):
     return t.data_ptr() if t is not None else None
 
 
-_BOUND_CACHE: dict = {}
-
-
 def _bound_rows(b) -> list:
-    """[[lo, hi]] * 3 as Python floats.  Device-resident bound tensors are cached by
-    (storage, version) so the per-call path never synchronises on a D2H copy."""
+    """[[lo, hi]] * 3 as Python floats.  For a device-resident bound the rows are
+    cached ON the tensor object, tagged with its storage pointer and version counter,
+    so the per-call path never synchronises on a D2H copy.  (A cache keyed by
+    data_ptr alone is wrong: the caching allocator hands freed addresses to new
+    tensors.)"""
     if isinstance(b, torch.Tensor):
-        key = (b.data_ptr(), b._version, b.device.type, tuple(b.shape))
-        hit = _BOUND_CACHE.get(key)
-        if hit is not None:
-            return hit
+        tag = (b.data_ptr(), b._version)
+        hit = getattr(b, "_nicecore_rows", None)
+        if hit is not None and hit[0] == tag:
+            return hit[1]
         t = b.detach().to("cpu", torch.float64).reshape(3, 2)
         rows = [[float(t[k, 0]), float(t[k, 1])] for k in range(3)]
-        if len(_BOUND_CACHE) > 64:
-            _BOUND_CACHE.clear()
-        _BOUND_CACHE[key] = rows
+        try:
+            b._nicecore_rows = (tag, rows)
+        except (AttributeError, RuntimeError):
+            pass
         return rows
     t = torch.as_tensor(b, dtype=torch.float64).reshape(3, 2)
     return [[float(t[k, 0]), float(t[k, 1])] for k in range(3)]
@@ -190,6 +191,7 @@ class NiceRenderFn(torch.autograd.Function):
         a.n_rays = N
         a.n_strat = spec["n_strat"]
         a.n_surf = spec["n_surf"]
+        a.flags = L.NC_SAVE_FOR_BACKWARD if any(ctx.needs_input_grad) else 0
         a.rays_o = rays_o.data_ptr()
         a.rays_d = rays_d.data_ptr()
         gt = None
@@ -286,6 +288,7 @@ class NiceEvalFn(torch.autograd.Function):
         a.abi_version = L.NC_ABI_VERSION
         a.stage = plan.stage
         a.n_points = P
+        a.flags = L.NC_SAVE_FOR_BACKWARD if any(ctx.needs_input_grad) else 0
         a.pts = pts.data_ptr()
         grids = (g0, g1, g2, g3)
         gkeep = []
