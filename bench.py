@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-oracle sample (0 disables)")
     ap.add_argument("--layout", default="channels_last", choices=["channels_last", "ncdhw"])
+    ap.add_argument("--eager", action="store_true",
+                    help="time the eager step instead of its hipGraph replay "
+                         "(nicecore.graph.GraphedStep)")
     return ap.parse_args()
 
 
@@ -99,20 +102,26 @@ def build_workload(args, rank, device):
 
 
 def make_step(w, args, world, device):
+    """One iteration = [all-reduce(MAX) of the depth bound] -> render_batch_ray ->
+    Mapper L1 loss -> backward -> [all-reduce of the gradients].  Returns the eager
+    step and the graph-replayed step (render + loss + backward captured once into a
+    hipGraph, nicecore.graph.GraphedStep; the collectives stay outside the graph)."""
     import torch.distributed as dist
     grids, model, renderer = w["grids"], w["model"], w["renderer"]
     ro, rd, gt, gtc = w["ro"], w["rd"], w["gt"], w["gtc"]
     params = [p for p in model.parameters() if p.requires_grad]
     gvals = [g for g in grids.values() if g.requires_grad]
     depth_mask = (gt > 0).double()
+    dmax = gt.max().reshape(1).clone() if world > 1 else None  # static buffer
 
-    def step():
+    def pre():
+        if world > 1:  # Renderer.py:157/:194 use max(gt_depth) over the whole (sharded) batch
+            torch.amax(gt, dim=0, keepdim=True, out=dmax)
+            dist.all_reduce(dmax, op=dist.ReduceOp.MAX)
+
+    def body():
         for t in params + gvals + [ro, rd]:
             t.grad = None
-        dmax = None
-        if world > 1:  # Renderer.py:157/:194 use max(gt_depth) over the whole (sharded) batch
-            dmax = gt.max().reshape(1)
-            dist.all_reduce(dmax, op=dist.ReduceOp.MAX)
         depth, unc, color = renderer.render_batch_ray(grids, model, rd, ro, device, args.stage,
                                                       gt, depth_max=dmax)
         # src/Mapper.py:603-612 (mask applied multiplicatively: same gradient, no host sync)
@@ -120,12 +129,30 @@ def make_step(w, args, world, device):
         if args.stage == "color":
             loss = loss + 0.2 * (gtc - color).abs().sum()
         loss.backward()
+        return loss
+
+    def post():
         if world > 1 and w["ba"]:
             hs = [dist.all_reduce(t.grad, async_op=True) for t in gvals + params if t.grad is not None]
             for h in hs:
                 h.wait()
-        return loss
-    return step
+
+    def eager():
+        pre()
+        body()
+        post()
+
+    graphed = None
+    if not args.eager:
+        from nicecore.graph import GraphedStep
+        pre()
+        g = GraphedStep(body)
+
+        def graphed():
+            pre()
+            g()
+            post()
+    return eager, graphed
 
 
 def algorithmic_flops_per_ray(stage, S, mode):
@@ -193,6 +220,16 @@ def read_traffic():
         return None
 
 
+class _NullTimer:
+    result = {}
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -200,24 +237,37 @@ def main():
     from nicecore import _lib as L
     L.load()
     w = build_workload(args, rank, device)
-    step = make_step(w, args, world, device)
+    eager, graphed = make_step(w, args, world, device)
     for _ in range(args.warmup):
-        step()
+        eager()
     torch.cuda.synchronize()
 
-    # per-kernel breakdown (separate pass, all kernels event-timed) -> dominant kernel
+    # per-kernel breakdown (separate eager pass, every library kernel event-timed on
+    # its launch stream) -> dominant kernel and its average launch duration
     with L.KernelTimer() as kt_all:
-        for _ in range(max(3, min(args.steps, 10))):
-            step()
+        for _ in range(max(5, min(args.steps, 20))):
+            eager()
     torch.cuda.synchronize()
     breakdown = {k: ms / n for k, (ms, n) in kt_all.result.items()}
     dominant = max(breakdown, key=breakdown.get)
 
+    # eager step time (reported beside the graph-replay value)
+    t0 = time.perf_counter()
+    for _ in range(max(5, min(args.steps, 20))):
+        eager()
+    torch.cuda.synchronize()
+    eager_ms = 1e3 * (time.perf_counter() - t0) / max(5, min(args.steps, 20))
+
+    step = graphed if graphed is not None else eager
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
     import torch.distributed as dist
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    with L.KernelTimer([dominant]) as kt:  # 2 event records per step, on the launch stream
+    timer = L.KernelTimer([dominant]) if graphed is None else _NullTimer()
+    with timer as kt:  # eager: 2 event records per step around the kernel, on its launch stream
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
@@ -229,7 +279,13 @@ def main():
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
-    ms_dom, n_dom = kt.result.get(dominant, (0.0, 0))
+    if graphed is None:
+        ms_dom, n_dom = kt.result.get(dominant, (0.0, 0))
+        timing_src = f"HIP events on the launch stream, {n_dom} launches in the timed region"
+    else:  # events inside a replayed graph keep only the last replay: use the eager pass
+        ms_dom, n_dom = kt_all.result.get(dominant, (0.0, 0))
+        timing_src = (f"HIP events on the launch stream, {n_dom} launches of the same step run "
+                      f"eagerly just before the graph-replay timed region")
     avg_ms = ms_dom / max(n_dom, 1)
 
     S = 48
@@ -242,8 +298,8 @@ def main():
         roof = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 3),
                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": (tr or {}).get(dominant), "avg_launch_ms": round(avg_ms, 4),
-                "flop_per_launch": fl}
+                "traffic": ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes"), "avg_launch_ms": round(avg_ms, 4),
+                "flop_per_launch": fl, "timing": timing_src}
 
     value = world * args.rays * args.steps / dt
     out = {
@@ -256,6 +312,8 @@ def main():
                    "rays_per_gpu": args.rays, "samples_per_ray": S, "stage": args.stage,
                    "mode": args.mode, "grid_layout": args.layout, "parallelism": f"dp{world}"},
         "roofline": roof,
+        "launch": "hipGraph replay" if graphed is not None else "eager",
+        "eager_ms_per_step": round(eager_ms, 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1])},
     }
     if world == 1 and rank == 0 and args.cpu_seconds > 0:

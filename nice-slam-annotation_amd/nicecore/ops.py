@@ -5,7 +5,6 @@ import torch
 
 from . import _lib as L
 from .render_fn import NiceEvalFn, NiceRenderFn, make_plan
-from .scene import linspace_tables
 
 
 def _grid_args(c):
@@ -35,7 +34,5 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     if n_strat + ns > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
         raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
-    t, ts = linspace_tables(n_strat, ns)
-    spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound,
-            "t_strat": t.tolist(), "t_surf": ts.tolist(), "depth_max": depth_max}
+    spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max}
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())

@@ -14,6 +14,7 @@ gradient and grid scatter).
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
@@ -110,8 +111,37 @@ def _decoder_bound(module, name):
     return b
 
 
+def _fast_decoder_params(module, kind: int):
+    """decoder_params() through the modules' own dicts (no ModuleList indexing):
+    the per-call validation path.  Falls back to attribute access."""
+    try:
+        mm = module._modules
+        ps = []
+        if kind != L.DEC_COARSE:
+            fc = mm["fc_c"]._modules
+            for i in ("0", "1", "2", "3", "4"):
+                q = fc[i]._parameters
+                ps += [q["weight"], q["bias"]]
+            emb = mm["embedder"]
+            B = emb._parameters.get("_B")
+            ps.append(B if B is not None else emb._B)
+        pl = mm["pts_linears"]._modules
+        for i in ("0", "1", "2", "3", "4"):
+            q = pl[i]._parameters
+            ps += [q["weight"], q["bias"]]
+        q = mm["output_linear"]._parameters
+        ps += [q["weight"], q["bias"]]
+        return ps
+    except (KeyError, AttributeError):
+        return decoder_params(module, kind)
+
+
 class _Plan:
-    """Which decoders / grids a stage touches and how the flat param list splits."""
+    """Binding of one (decoders module, stage): which decoders / grids the stage
+    touches, the decoder parameters in ABI order, and a pre-filled ctypes image of
+    the decoder pointer tables.  Cached per decoders object (``make_plan``) and
+    re-validated on every call by object identity + storage pointer + bound tag,
+    so a replaced parameter, a ``.data`` swap or a new bound rebuilds it."""
 
     def __init__(self, stage: int, decoders):
         self.stage = stage
@@ -124,20 +154,90 @@ class _Plan:
                 raise L.NiceCoreError(f"stage needs the {L.DECODER_NAMES[k]} decoder")
         self.params = {k: decoder_params(self.modules[k], k) for k in self.decs}
         self.bounds = {k: _decoder_bound(self.modules[k], L.DECODER_NAMES[k]) for k in self.decs}
+        self._flat = tuple(p for k in self.decs for p in self.params[k])
+        sl, o = {}, 0
+        for k in self.decs:
+            sl[k] = (o, o + len(self.params[k]))
+            o += len(self.params[k])
+        self._slices = sl
+        self._sig = None
+        self._dec_img = None
+        self._templates = {}
 
     def flat_params(self):
-        out = []
-        for k in self.decs:
-            out += self.params[k]
-        return out
+        return list(self._flat)
 
     def param_slices(self):
-        s, o = {}, 0
+        return self._slices
+
+    def _signature(self):
+        bt = []
         for k in self.decs:
-            n = len(self.params[k])
-            s[k] = (o, o + n)
-            o += n
-        return s
+            b = self.bounds[k]
+            bt.append((b.data_ptr(), b._version) if isinstance(b, torch.Tensor) else id(b))
+        return tuple(p.data_ptr() for p in self._flat), tuple(bt)
+
+    def still_valid(self, decoders) -> bool:
+        mods = decoder_modules(decoders)
+        for k in self.decs:
+            m = mods[k]
+            if m is not self.modules[k] or getattr(m, "bound", None) is not self.bounds[k]:
+                return False
+            cur = _fast_decoder_params(m, k)
+            old = self.params[k]
+            if len(cur) != len(old) or any(a is not b for a, b in zip(cur, old)):
+                return False
+        return True
+
+    def decoder_image(self, device):
+        """(NcDecoderParams * 4) with the pointers / bounds filled (grad = NULL)."""
+        sig = self._signature()
+        if sig != self._sig or self._dec_img is None:
+            img = (L.NcDecoderParams * 4)()
+            for k in self.decs:
+                _fill_decoder(img[k], k, self.params[k], self.bounds[k], device)
+            self._dec_img, self._sig = img, sig
+            self._templates.clear()
+        return self._dec_img
+
+    def render_template(self, device, n_strat, n_surf, bound):
+        """NcRenderArgs with every per-plan field filled; per call the caller copies
+        it (from_buffer_copy) and sets the tensors."""
+        img = self.decoder_image(device)
+        bkey = (bound.data_ptr(), bound._version) if isinstance(bound, torch.Tensor) else id(bound)
+        key = ("render", n_strat, n_surf, bkey)
+        t = self._templates.get(key)
+        if t is None:
+            from .scene import linspace_tables
+            ts, tsurf = linspace_tables(n_strat, n_surf)
+            t = L.NcRenderArgs()
+            t.abi_version = L.NC_ABI_VERSION
+            t.stage = self.stage
+            t.n_strat, t.n_surf = n_strat, n_surf
+            rows = _bound_rows(bound)
+            for k in range(3):
+                t.bound[k][0], t.bound[k][1] = rows[k]
+            for k, v in enumerate(ts.tolist()):
+                t.t_strat[k] = v
+            for k, v in enumerate(tsurf.tolist()):
+                t.t_surf[k] = v
+            ctypes.memmove(ctypes.addressof(t.dec), ctypes.addressof(img), ctypes.sizeof(img))
+            self._templates[key] = t
+        return t
+
+    def points_template(self, device):
+        img = self.decoder_image(device)
+        t = self._templates.get("points")
+        if t is None:
+            t = L.NcPointsArgs()
+            t.abi_version = L.NC_ABI_VERSION
+            t.stage = self.stage
+            ctypes.memmove(ctypes.addressof(t.dec), ctypes.addressof(img), ctypes.sizeof(img))
+            self._templates["points"] = t
+        return t
+
+
+_PLANS = weakref.WeakKeyDictionary()  # decoders module -> {stage: _Plan}
 
 
 def _alloc_param_grads(lib, plan, needs_params, args, device):
@@ -185,13 +285,10 @@ class NiceRenderFn(torch.autograd.Function):
         rays_o = rays_o.detach().float().contiguous()
         rays_d = rays_d.detach().float().contiguous()
         N = rays_o.shape[0]
-        a = L.NcRenderArgs()
-        a.abi_version = L.NC_ABI_VERSION
-        a.stage = plan.stage
-        a.n_rays = N
-        a.n_strat = spec["n_strat"]
-        a.n_surf = spec["n_surf"]
+        a = L.NcRenderArgs.from_buffer_copy(
+            plan.render_template(device, spec["n_strat"], spec["n_surf"], spec["bound"]))
         a.flags = L.NC_SAVE_FOR_BACKWARD if any(ctx.needs_input_grad) else 0
+        a.n_rays = N
         a.rays_o = rays_o.data_ptr()
         a.rays_d = rays_d.data_ptr()
         gt = None
@@ -202,14 +299,6 @@ class NiceRenderFn(torch.autograd.Function):
         if dmax is not None:
             dmax = dmax.detach().reshape(1).float().contiguous()
             a.depth_max = dmax.data_ptr()
-        rows = _bound_rows(spec["bound"])
-        for k in range(3):
-            a.bound[k][0], a.bound[k][1] = rows[k]
-        ts, tsurf = spec["t_strat"], spec["t_surf"]
-        for k in range(len(ts)):
-            a.t_strat[k] = float(ts[k])
-        for k in range(len(tsurf)):
-            a.t_surf[k] = float(tsurf[k])
         grids = (g0, g1, g2, g3)
         gkeep = []
         for k in plan.grids:
@@ -218,8 +307,6 @@ class NiceRenderFn(torch.autograd.Function):
             g = grids[k].detach()
             _fill_grid(a.grids[k], g, device)
             gkeep.append(g)
-        for k in plan.decs:
-            _fill_decoder(a.dec[k], k, plan.params[k], plan.bounds[k], device)
         depth = torch.empty(N, device=device, dtype=torch.float64)
         var = torch.empty(N, device=device, dtype=torch.float64)
         color = torch.empty(N, 3, device=device, dtype=torch.float32)
@@ -284,9 +371,7 @@ class NiceEvalFn(torch.autograd.Function):
             raise L.NiceCoreError("nicecore evaluates on a HIP device; points are on " + str(device))
         pts = p.detach().reshape(-1, 3).double().contiguous()
         P = pts.shape[0]
-        a = L.NcPointsArgs()
-        a.abi_version = L.NC_ABI_VERSION
-        a.stage = plan.stage
+        a = L.NcPointsArgs.from_buffer_copy(plan.points_template(device))
         a.n_points = P
         a.flags = L.NC_SAVE_FOR_BACKWARD if any(ctx.needs_input_grad) else 0
         a.pts = pts.data_ptr()
@@ -298,8 +383,6 @@ class NiceEvalFn(torch.autograd.Function):
             g = grids[k].detach()
             _fill_grid(a.grids[k], g, device)
             gkeep.append(g)
-        for k in plan.decs:
-            _fill_decoder(a.dec[k], k, plan.params[k], plan.bounds[k], device)
         raw = torch.empty(P, 4, device=device, dtype=torch.float32)
         a.raw = raw.data_ptr()
         nbytes = lib.nc_points_workspace_bytes(ctypes.byref(a))
@@ -345,4 +428,15 @@ class NiceEvalFn(torch.autograd.Function):
 
 def make_plan(stage, decoders) -> _Plan:
     s = L.STAGES[stage] if isinstance(stage, str) else int(stage)
-    return _Plan(s, decoders)
+    try:
+        per = _PLANS.get(decoders)
+    except TypeError:  # not weak-referenceable: no caching
+        return _Plan(s, decoders)
+    if per is None:
+        per = {}
+        _PLANS[decoders] = per
+    plan = per.get(s)
+    if plan is None or not plan.still_valid(decoders):
+        plan = _Plan(s, decoders)
+        per[s] = plan
+    return plan

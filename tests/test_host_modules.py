@@ -51,3 +51,59 @@ def test_synth_rays_pass_bbox_filter():
     t = S.ray_exit_t(sc.bound, ro, rd)
     assert bool((t >= dep.double()).all())
     assert (dep == 0).float().mean() > 0.03
+
+
+def _model_with_bounds():
+    m = D.build_default_nice(seed=0)
+    b = S.make_scene("tiny").bound
+    m.bound = b
+    for n in ("middle", "fine", "color"):
+        getattr(m, n + "_decoder").bound = b
+    m.coarse_decoder.bound = b * 2
+    return m
+
+
+def test_plan_cache_reuse_and_invalidation():
+    """The per-decoders binding is reused while the parameters are the same objects
+    and storage, and rebuilt when a parameter object, its storage or a bound changes."""
+    from nicecore import _lib as L
+    from nicecore.render_fn import make_plan, decoder_params
+    m = _model_with_bounds()
+    p1 = make_plan("color", m)
+    assert make_plan("color", m) is p1
+    assert make_plan("middle", m) is not p1
+    # ABI order == decoder_params == fast path
+    for k in p1.decs:
+        assert all(a is b for a, b in zip(p1.params[k], decoder_params(p1.modules[k], k)))
+    img = p1.decoder_image(torch.device("cpu"))
+    w0 = m.fine_decoder.pts_linears[0].weight
+    assert img[L.DEC_FINE].lin_w[0] == w0.data_ptr()
+    # .data swap keeps the object but moves the storage -> image refreshed
+    w0.data = w0.data.clone()
+    img2 = p1.decoder_image(torch.device("cpu"))
+    assert make_plan("color", m) is p1
+    assert img2[L.DEC_FINE].lin_w[0] == w0.data_ptr()
+    # a replaced Parameter object -> new plan
+    m.fine_decoder.pts_linears[0].weight = torch.nn.Parameter(w0.detach().clone())
+    p2 = make_plan("color", m)
+    assert p2 is not p1
+    assert p2.params[L.DEC_FINE][11] is m.fine_decoder.pts_linears[0].weight
+    # a new bound object -> new plan
+    m.fine_decoder.bound = m.fine_decoder.bound.clone()
+    assert make_plan("color", m) is not p2
+
+
+def test_render_template_fields():
+    from nicecore import _lib as L
+    from nicecore.render_fn import make_plan
+    m = _model_with_bounds()
+    plan = make_plan("color", m)
+    b = m.bound
+    t = plan.render_template(torch.device("cpu"), 32, 16, b)
+    assert t.abi_version == L.NC_ABI_VERSION and t.stage == 3 and (t.n_strat, t.n_surf) == (32, 16)
+    ts, tsurf = S.linspace_tables(32, 16)
+    assert [t.t_strat[k] for k in range(32)] == ts.tolist()
+    assert [t.t_surf[k] for k in range(16)] == tsurf.tolist()
+    assert t.bound[0][1] == float(b[0, 1])
+    assert t.dec[L.DEC_COLOR].out_w == m.color_decoder.output_linear.weight.data_ptr()
+    assert plan.render_template(torch.device("cpu"), 32, 16, b) is t

@@ -1,0 +1,43 @@
+"""Per-kernel HBM traffic per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+passes (separate runs; tools/prof_session.sh), with the gfx950 correction of
+MI355X_MICROARCH.md § HBM: FETCH_SIZE counts half the bytes of wide coalesced
+reads (x2); WRITE_SIZE is exact for 16-B stores and float atomics.
+FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB.
+
+    python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json]
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r["Kernel_Name"]
+        if not name.startswith("nc::"):
+            continue
+        acc[name.split("(")[0].replace("nc::", "")].append(float(r["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+
+if __name__ == "__main__":
+    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f_kib, nf = fetch.get(k, (0.0, 0))
+        w_kib, nw = write.get(k, (0.0, 0))
+        rd = 2.0 * f_kib * 1024
+        wr = w_kib * 1024
+        out[k] = {"hbm_bytes": round(rd + wr), "read_bytes_corrected": round(rd), "write_bytes": round(wr),
+                  "fetch_size_kib_raw": round(f_kib, 1), "write_size_kib_raw": round(w_kib, 1),
+                  "launches": [nf, nw]}
+        print(f"{k:22s} read {rd / 1e6:9.2f} MB  write {wr / 1e6:9.2f} MB  ({nf}/{nw} launches)")
+    if len(sys.argv) > 3:
+        json.dump({"note": "HBM bytes per launch, rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) "
+                           "and WRITE_SIZE in separate passes; see tools/pmc_traffic.py",
+                   "kernels": out}, open(sys.argv[3], "w"), indent=1)
