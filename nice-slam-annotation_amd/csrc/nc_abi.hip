@@ -182,7 +182,9 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
     w.drec = take((size_t)d * 4);
   }
   const int64_t blocks = (P + 31) / 32;  // k_mlp_dw sub-chunks
-  int per_job = (cu_count() + pl.n_jobs - 1) / pl.n_jobs;
+  // one wave of resident workgroups over all jobs (floor: a 257th workgroup on a
+  // 256-CU chip would run as a second, serial round)
+  int per_job = cu_count() * mlp_blocks_per_cu(2) / pl.n_jobs;
   if (per_job < 1) per_job = 1;
   w.slab_wgs = (int)((blocks < per_job) ? (blocks > 0 ? blocks : 1) : per_job);
   w.slab_stride = (max_param_count() + 63) & ~int64_t(63);
@@ -284,10 +286,11 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
   c.g_rays_d = a->g_rays_d;
 }
 
-int fwd_grid_x(int64_t P, int n_jobs) {
-  const int64_t per = FWD_THREADS / 64 * 16;
+int fwd_grid_x(int64_t P, int n_jobs, int which = 0) {
+  const int64_t per = (which == 0 ? FWD_THREADS : DX_THREADS) / 64 * 16;
   const int64_t blocks = (P + per - 1) / per;
-  int x = (cu_count() + n_jobs - 1) / n_jobs;
+  int x = cu_count() * mlp_blocks_per_cu(which) / n_jobs;
+  if (x < 1) x = 1;
   if (blocks < x) x = (int)(blocks > 0 ? blocks : 1);
   return x;
 }
@@ -308,7 +311,7 @@ int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s);
 // backward -> weight gradients -> slab reduction
 int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s) {
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
-  if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs), s); }), "k_mlp_dx")) return e;
+  if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs, 1), s); }), "k_mlp_dx")) return e;
   if (int e = check_hip(timed(KID_GRID_BWD, s, [&] { return launch_grid_bwd(m, s); }), "k_grid_bwd")) return e;
   bool any_dw = false;
   for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;

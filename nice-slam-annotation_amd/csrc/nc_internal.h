@@ -110,6 +110,7 @@ int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s);
 
 int mlp_fwd_lds_bytes();
 int mlp_dw_lds_bytes();
+int mlp_blocks_per_cu(int which);  // 0 k_mlp_fwd, 1 k_mlp_dx, 2 k_mlp_dw
 int rec_len(int kind);   // floats per point of a decoder's forward record
 int drec_len(int kind);  // ... and of its backward record
 int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);

@@ -755,6 +755,30 @@ static int set_lds(K kernel, int bytes) {
   return (int)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
+// resident workgroups per CU of k_mlp_fwd (0), k_mlp_dx (1), k_mlp_dw (2), from the
+// HIP occupancy calculator (registers, LDS, wave slots); cached per device
+int mlp_blocks_per_cu(int which) {
+  static int cache[64][3] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || which < 0 || which > 2) return 1;
+  if (!cache[dev][which]) {
+    int n = 0;
+    hipError_t e = hipSuccess;
+    if (which == 0) {
+      set_lds(k_mlp_fwd, mlp_fwd_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd, FWD_THREADS, mlp_fwd_lds_bytes());
+    } else if (which == 1) {
+      set_lds(k_mlp_dx, mlp_fwd_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dx, DX_THREADS, mlp_fwd_lds_bytes());
+    } else {
+      set_lds(k_mlp_dw, mlp_dw_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dw, DW_THREADS, mlp_dw_lds_bytes());
+    }
+    cache[dev][which] = (e == hipSuccess && n > 0) ? n : 1;
+  }
+  return cache[dev][which];
+}
+
 int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s) {
   static int attr = -1;
   if (attr != 0 && (attr = set_lds(k_mlp_fwd, mlp_fwd_lds_bytes())) != 0) return attr;

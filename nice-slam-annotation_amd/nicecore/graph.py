@@ -23,6 +23,16 @@ from __future__ import annotations
 import torch
 
 
+def _detach(out):
+    """Outputs are kept detached: a live loss would keep the autograd graph of the
+    previous iteration (and its AccumulateGrad nodes) alive across replays."""
+    if isinstance(out, torch.Tensor):
+        return out.detach()
+    if isinstance(out, (tuple, list)):
+        return type(out)(_detach(o) for o in out)
+    return out
+
+
 class GraphedStep:
     def __init__(self, body, warmup: int = 3, pool=None):
         self.body = body
@@ -30,12 +40,12 @@ class GraphedStep:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm up allocator / autograd outside capture
             for _ in range(warmup):
-                self.out = body()
+                _detach(body())
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
-            self.out = body()
+            self.out = _detach(body())
 
     def __call__(self):
         self.graph.replay()
