@@ -144,8 +144,8 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, rec = 0, drec = 0, total = 0;
-  int64_t rec_off[MAX_JOBS] = {0, 0, 0}, drec_off[MAX_JOBS] = {0, 0, 0};
+  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, rec = 0, total = 0;
+  int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
   int slab_wgs = 1;
   int64_t slab_stride = 0;
@@ -171,15 +171,12 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
   w.dcbuf = take((size_t)pl.n_jobs * P * 32 * 4);
   w.save = save;
   if (save) {
-    int64_t r = 0, d = 0;
+    int64_t r = 0;
     for (int j = 0; j < pl.n_jobs; ++j) {
       w.rec_off[j] = r;
-      w.drec_off[j] = d;
-      r += P * rec_len(pl.jobs[j].kind);
-      d += P * drec_len(pl.jobs[j].kind);
+      r += P * rec_stride(pl.jobs[j].kind);
     }
     w.rec = take((size_t)r * 4);
-    w.drec = take((size_t)d * 4);
   }
   const int64_t blocks = (P + 31) / 32;  // k_mlp_dw sub-chunks
   // one wave of resident workgroups over all jobs (floor: a 257th workgroup on a
@@ -209,7 +206,6 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   for (int j = 0; j < pl.n_jobs; ++j) {
     m.jobs[j] = pl.jobs[j];
     m.jobs[j].rec_off = w.rec_off[j];
-    m.jobs[j].drec_off = w.drec_off[j];
     const int k = pl.jobs[j].kind;
     m.jobs[j].need_dw = dec[k].grad != nullptr;
     m.jobs[j].need_grid = grids[k].grad != nullptr;
@@ -228,7 +224,6 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.dcbuf = at<float>(ws, w.dcbuf);
   m.slab = at<float>(ws, w.slab);
   m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
-  m.drec = w.save ? at<float>(ws, w.drec) : nullptr;
 }
 
 int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S) {

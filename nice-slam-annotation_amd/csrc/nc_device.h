@@ -45,7 +45,16 @@ __device__ __forceinline__ int feat_of(int j, int g) { return 16 * (j >> 2) + 4 
 //     L3 (coarse, MLP_no_xyz): c 0..31 | h2 32..63      -> 64
 //   Flat parameter vector (gradient output): nn.Module.parameters() order.
 // ---------------------------------------------------------------------------
-template <int KIND>
+// PADW: row padding of the LDS weight images (LD = K + PADW floats).  The forward
+// reads weights with ds_read_b128 (lane (i, g) at row i, column 4g): its four
+// 16-lane groups {0-3,12-15,20-27}, ... hit 16 distinct 16-B slots iff
+// LD/4 == 2 (mod 4), i.e. PADW = 8 for every K here (96, 32, 128, 64).  The dX
+// kernel reads the transposed rows with ds_read_b32 (32-bank halves; rows 4 apart
+// per lane group) and needs LD == 4 (mod 16): PADW = 4.
+constexpr int PADW_FWD = 8;
+constexpr int PADW_BWD = 4;
+
+template <int KIND, int PADW = PADW_BWD>
 struct Net {
   static constexpr bool XYZ = KIND != K_COARSE;
   static constexpr int CD = (KIND == K_FINE) ? 64 : 32;   // fc_c input width
@@ -58,7 +67,7 @@ struct Net {
   // packed input widths
   static constexpr int IN0 = XYZ ? EMBP : HID;
   static constexpr int IN3 = XYZ ? (EMBP + HID) : (2 * HID);
-  static constexpr int LD0 = IN0 + 4, LDH = HID + 4, LD3 = IN3 + 4, LDC = CD + 4;
+  static constexpr int LD0 = IN0 + PADW, LDH = HID + PADW, LD3 = IN3 + PADW, LDC = CD + PADW;
   // LDS offsets (floats)
   static constexpr int W0 = 0;
   static constexpr int W1 = W0 + HID * LD0;
@@ -196,6 +205,27 @@ __device__ __forceinline__ bool grid_vec_ok(const nc_grid& G) {
 __device__ __forceinline__ void normalize_pt(const double p[3], const double (&b)[3][2], float out[3]) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) out[k] = (float)(((p[k] - b[k][0]) / (b[k][1] - b[k][0])) * 2.0 - 1.0);
+}
+
+// sin / cos of the Fourier-feature arguments x = p.float() @ B (decoder.py:26-30;
+// |x| reaches ~1e3 rad for room-scale scenes with B ~ N(0, 25^2)).  Cody-Waite
+// reduction of x to [-pi, pi] with a three-part 2*pi, then the hardware
+// v_sin_f32 / v_cos_f32 on the reduced argument in revolutions: 6 VALU instead of
+// ocml's polynomial + Payne-Hanek path.  Measured against float64 over
+// |x| <= 1e3 (tools/sin_accuracy.hip): max abs error 3.8e-7 (ocml sinf 6.8e-8,
+// __sinf 8.8e-5).  The same function is used wherever a feature is recomputed, so
+// forward and backward see identical values.
+__device__ __forceinline__ float reduce_2pi(float x) {
+  const float k = __builtin_rintf(x * 0.15915494309189535f);
+  float r = __builtin_fmaf(-k, 6.28125f, x);
+  r = __builtin_fmaf(-k, 1.9353071795864769e-3f, r);
+  return __builtin_fmaf(-k, 1.2537033403800354e-11f, r);
+}
+__device__ __forceinline__ float fourier_sin(float x) {
+  return __builtin_amdgcn_sinf(reduce_2pi(x) * 0.15915494309189535f);
+}
+__device__ __forceinline__ float fourier_cos(float x) {
+  return __builtin_amdgcn_cosf(reduce_2pi(x) * 0.15915494309189535f);
 }
 
 // Wavefront reductions over the four lanes of a point (lane-groups g).

@@ -17,8 +17,8 @@ struct Job {
   int32_t need_grid;   // gradient into its own grid (the fine decoder's middle lookup never has one)
   int32_t need_coord;  // gradient into the sample points
   int32_t pad;
-  int64_t rec_off;     // float offset of this job's forward records in MlpCtx::rec
-  int64_t drec_off;    // float offset of its backward records in MlpCtx::drec
+  int64_t rec_off;     // float offset of this job's point records in MlpCtx::rec
+  int64_t pad2;
 };
 
 constexpr int MAX_JOBS = 3;
@@ -42,8 +42,8 @@ struct MlpCtx {
   const float* grgb;         // [P][3] d loss / d rgb
   double* dpts;              // [n_jobs][P][3] per-decoder point gradients
   float* dcbuf;              // [n_jobs][P][32] d loss / d own-grid features (k_mlp_dx -> k_grid_bwd)
-  float* rec;                // per job [P][Rec::LEN]  forward activations (k_mlp_fwd -> dx, dw)
-  float* drec;               // per job [P][Rec::DLEN] backward activations (k_mlp_dx -> k_mlp_dw)
+  float* rec;                // per job [P][Rec::STRIDE]: forward activations (k_mlp_fwd) followed
+                             // by backward activations (k_mlp_dx); both read by k_mlp_dw
   float* slab;               // [n_jobs][slab_wgs][slab_stride] per-workgroup parameter gradients
   int64_t slab_stride;
 };
@@ -111,8 +111,7 @@ int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s);
 int mlp_fwd_lds_bytes();
 int mlp_dw_lds_bytes();
 int mlp_blocks_per_cu(int which);  // 0 k_mlp_fwd, 1 k_mlp_dx, 2 k_mlp_dw
-int rec_len(int kind);   // floats per point of a decoder's forward record
-int drec_len(int kind);  // ... and of its backward record
+int rec_stride(int kind);  // floats per point of a decoder's [forward | backward] record
 int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dw(const MlpCtx& c, hipStream_t s);

@@ -27,15 +27,12 @@
 #include "nc_device.h"
 #include "nc_internal.h"
 
-#ifdef NC_ABL_FAST_TRIG  // timing-only ablation: hardware sin/cos (wrong for large arguments)
-#define NC_SIN __sinf
-#define NC_COS __cosf
-#elif defined(NC_ABL_NO_TRIG)  // timing-only ablation: no trig at all
+#ifdef NC_ABL_NO_TRIG  // timing-only ablation: no trig at all
 #define NC_SIN(x) (x)
 #define NC_COS(x) (x)
 #else
-#define NC_SIN sinf
-#define NC_COS cosf
+#define NC_SIN fourier_sin
+#define NC_COS fourier_cos
 #endif
 
 namespace nc {
@@ -43,9 +40,9 @@ namespace nc {
 // ---------------------------------------------------------------------------
 // weights: nn.Parameter storage -> LDS image (layout: Net<KIND>)
 // ---------------------------------------------------------------------------
-template <int KIND>
+template <int KIND, int PADW>
 __device__ __forceinline__ void load_weights(float* lds, const nc_decoder_params& P) {
-  using N = Net<KIND>;
+  using N = Net<KIND, PADW>;
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int e = tid; e < N::WEIGHTS; e += nt) lds[e] = 0.f;
   __syncthreads();
@@ -140,7 +137,7 @@ __device__ __forceinline__ bool mask_bit(unsigned lo, unsigned hi, int L, int j)
 template <int KIND>
 __device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx, int slot, int64_t p,
                                              bool valid, int i, int g, WaveRegs<KIND>& R, float out[4]) {
-  using N = Net<KIND>;
+  using N = Net<KIND, PADW_FWD>;
   // grid features (decoder.py:179-188 / :196-202); coordinates normalised once per
   // point by k_ray_setup / k_points_prep
   float xyz[3];
@@ -242,21 +239,24 @@ __device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx
 // ---------------------------------------------------------------------------
 // Per-point activation record saved by the forward for the backward kernels
 // (float offsets; every block starts on a 16-byte boundary):
-//   [emb 96 (xyz decoders)] [h_0..h_4 5x32] [c CD] [relu masks: lane-group g -> u32 lo, hi]
-// Backward record written by k_mlp_dx: [dh_0..dh_4 5x32] [dx 96 (xyz)] where dh_L is
+//   [h_0..h_4 5x32] [c CD] [relu masks: lane-group g -> u32 lo, hi]
+// The Fourier features are not stored: k_mlp_dw recomputes them from p.float()
+// with the forward's own fourier_sin (bit-identical, ~110 MB less traffic a step).
+// Backward record written by k_mlp_dx right after it (same point, offset LEN):
+// [dh_0..dh_4 5x32] [dx 96 (xyz)] where dh_L is
 // d loss / d h_L (block L's output) and dx = d loss / d (p @ B).
 // ---------------------------------------------------------------------------
 template <int KIND>
 struct Rec {
   using N = Net<KIND>;
-  static constexpr int EMB = 0;
-  static constexpr int H = N::XYZ ? EMBP : 0;
+  static constexpr int H = 0;
   static constexpr int C = H + 5 * HID;
   static constexpr int M = C + N::CD;
   static constexpr int LEN = M + 8;
   static constexpr int DH = 0;
   static constexpr int DX = 5 * HID;
   static constexpr int DLEN = DX + (N::XYZ ? EMBP : 0);
+  static constexpr int STRIDE = LEN + DLEN;  // one point: [forward record | backward record]
 };
 
 template <int NT>
@@ -269,7 +269,6 @@ __device__ __forceinline__ void store_rows(float* dst, const float* v, int g) {
 template <int KIND>
 __device__ __forceinline__ void save_record(float* r, const WaveRegs<KIND>& R, int g) {
   using RC = Rec<KIND>;
-  if constexpr (Net<KIND>::XYZ) store_rows<6>(r + RC::EMB, R.emb, g);
 #pragma unroll
   for (int L = 0; L < 5; ++L) store_rows<2>(r + RC::H + HID * L, R.h[L], g);
   store_rows<Net<KIND>::CD / 16>(r + RC::C, R.c, g);
@@ -287,7 +286,7 @@ __device__ __forceinline__ Job pick_job(const Job (&jobs)[MAX_JOBS], unsigned y)
 // ---------------------------------------------------------------------------
 template <int KIND>
 __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float* lds) {
-  load_weights<KIND>(lds, ctx.dec[KIND]);
+  load_weights<KIND, PADW_FWD>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
   const int64_t per = 16 * waves;
@@ -301,7 +300,7 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     WaveRegs<KIND> R;
     float out[4];
     wave_forward<KIND>(lds, ctx, job.slot, p, valid, i, g, R, out);
-    if (ctx.save_rec && valid) save_record<KIND>(ctx.rec + job.rec_off + p * Rec<KIND>::LEN, R, g);
+    if (ctx.save_rec && valid) save_record<KIND>(ctx.rec + job.rec_off + p * Rec<KIND>::STRIDE, R, g);
     if (valid && g == 0) {
       if constexpr (KIND == K_COLOR) {
         ctx.rgb[p * 3 + 0] = out[0];
@@ -362,7 +361,7 @@ template <int KIND>
 __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float* lds) {
   using N = Net<KIND>;
   using RC = Rec<KIND>;
-  load_weights<KIND>(lds, ctx.dec[KIND]);
+  load_weights<KIND, PADW_BWD>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
   const bool need_dw = job.need_dw != 0;
@@ -374,8 +373,8 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
     asm volatile("" ::: "memory");  // keep LDS weight reads inside the loop (see fwd_job)
     const int64_t p = t * 16 + i;
     const bool valid = p < ctx.P;
-    const float* rec = ctx.rec + job.rec_off + (valid ? p : 0) * RC::LEN;
-    float* drec = ctx.drec + job.drec_off + (valid ? p : 0) * RC::DLEN;
+    float* rec = ctx.rec + job.rec_off + (valid ? p : 0) * RC::STRIDE;
+    float* drec = rec + RC::LEN;
     float dout[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned mlo = 0, mhi = 0;
     if (valid) {
@@ -490,19 +489,27 @@ __global__ void __launch_bounds__(DX_THREADS) k_mlp_dx(const MlpCtx ctx) {
 // registers; bias gradients (row sums of dY) go to LDS float atomics.  One flush
 // per workgroup into a slab, summed by k_param_reduce.
 // ---------------------------------------------------------------------------
-constexpr int DW_NPTS = 32;
+constexpr int DW_NPTS = 32;  // points per staged sub-chunk (8 MFMA k-steps)
 
 template <int KIND>
 struct DwLayout {
   using RC = Rec<KIND>;
-  static constexpr int DREC = RC::LEN;           // backward record follows the forward one
+  // row: [emb 96 (xyz decoders, recomputed)] [forward record] [backward record] [pf] [d out]
+  static constexpr int EMB = 0;
+  static constexpr int REC0 = Net<KIND>::XYZ ? EMBP : 0;
+  static constexpr int H = REC0 + RC::H;
+  static constexpr int C = REC0 + RC::C;
+  static constexpr int M = REC0 + RC::M;
+  static constexpr int DREC = REC0 + RC::LEN;    // backward record follows the forward one
   static constexpr int PF = DREC + RC::DLEN;     // p.float() (4)
   static constexpr int DOUT = PF + 4;            // d out (4; rows >= NOUT zero)
-  static constexpr int RS = DOUT + 4;            // row stride (== 16 mod 32)
+  static constexpr int DZ = DOUT + 4;            // dZ_L = dh_L * relu'(Z_L), 5 x 32 (staged)
+  static constexpr int RS = DZ + 5 * HID;        // row stride (== 16 mod 32)
   static constexpr int BUF = DW_NPTS * RS;
   static constexpr int BACC = BUF;               // bias accumulators after the buffer
   static constexpr int BACC_FLOATS = 16 + 32 * 10;
-  static constexpr int TOTAL = BACC + BACC_FLOATS;
+  static constexpr int FB = BACC + BACC_FLOATS;  // Fourier B [3][96] (xyz decoders)
+  static constexpr int TOTAL = FB + 3 * EMBP;
   static_assert(RS % 32 == 16, "row stride must be 16 mod 32 for conflict-free operand reads");
 };
 
@@ -558,63 +565,81 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
   float* buf = lds;
   float* bacc = lds + LY::BACC;
   for (int e = threadIdx.x; e < LY::BACC_FLOATS; e += blockDim.x) bacc[e] = 0.f;
+  if constexpr (N::XYZ) {
+    const float* Bsrc = KIND == K_MID ? ctx.dec[K_MID].fourier_B
+                        : KIND == K_FINE ? ctx.dec[K_FINE].fourier_B : ctx.dec[K_COLOR].fourier_B;
+    for (int e = threadIdx.x; e < 3 * EMBP; e += blockDim.x) {
+      const int k = e / EMBP, m = e - k * EMBP;
+      lds[LY::FB + e] = m < EMB ? Bsrc[k * EMB + m] : 0.f;
+    }
+  }
   floatx4 acc[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) acc[s] = zero4();
   // Per-tile operand descriptors.  The k-step is branch-free: a dY column that does
-  // not exist (output rows >= NOUT) and the Fourier tile's x columns >= 3 read the
-  // always-zero DOUT+3 slot, and tiles without a relu mask test bit 0 of the
-  // all-ones PF+3 slot.
+  // not exist (output rows >= NOUT), the Fourier tile's x columns >= 3 and padding
+  // slots read the always-zero DOUT+3 slot; relu masks are pre-applied (DZ).
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  unsigned dyx[NS], dm[NS];  // yoff | xoff << 16,  mword | (1 << mbit) bit position << 16
+  // operand row pointers (lane-group g's point row; k-step q adds 4 rows) and mask bit
+  int yrow[NS], xrow[NS];  // float offsets into buf (32-bit LDS addresses)
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int tau = wv + DW_WAVES * s;
     int ph, to, ti;
     TL::get(tau < TL::NT ? tau : 0, ph, to, ti);
     const int o = 16 * to + i;
-    int yoff, xoff, mword = LY::PF + 3, mbit = 0;
+    int yoff, xoff;
     if (ph == 0) {
       yoff = LY::DOUT + (o < N::NOUT ? o : 3);
-      xoff = RC::H + HID * 4 + 16 * ti + i;
+      xoff = LY::H + HID * 4 + 16 * ti + i;
     } else if (ph <= 5) {
       const int L = 5 - ph;
-      yoff = LY::DREC + RC::DH + HID * L + o;
-      mword = RC::M + 2 * ((o >> 2) & 3) + (L == 4 ? 1 : 0);
-      mbit = (L == 4 ? 0 : 8 * L) + 4 * (o >> 4) + (o & 3);
+      yoff = LY::DZ + HID * L + o;
       const int c = 16 * ti + i;
-      if (L == 0) xoff = N::XYZ ? RC::EMB + c : RC::C + c;
-      else if (L == 3) xoff = N::XYZ ? (c < EMBP ? RC::EMB + c : RC::H + HID * 2 + (c - EMBP))
-                                     : (c < HID ? RC::C + c : RC::H + HID * 2 + (c - HID));
-      else xoff = RC::H + HID * (L - 1) + c;
+      if (L == 0) xoff = N::XYZ ? LY::EMB + c : LY::C + c;
+      else if (L == 3) xoff = N::XYZ ? (c < EMBP ? LY::EMB + c : LY::H + HID * 2 + (c - EMBP))
+                                     : (c < HID ? LY::C + c : LY::H + HID * 2 + (c - HID));
+      else xoff = LY::H + HID * (L - 1) + c;
     } else if (ph <= 10) {
       yoff = LY::DREC + RC::DH + HID * (10 - ph) + o;
-      xoff = RC::C + 16 * ti + i;
+      xoff = LY::C + 16 * ti + i;
     } else {
       yoff = LY::DREC + RC::DX + o;
       xoff = i < 3 ? LY::PF + i : LY::DOUT + 3;
     }
-    dyx[s] = (unsigned)yoff | ((unsigned)xoff << 16);
-    dm[s] = (unsigned)mword | ((unsigned)mbit << 16);
+    if (tau >= TL::NT) yoff = xoff = LY::DOUT + 3;  // padding slot: zero operands, never flushed
+    yrow[s] = g * LY::RS + yoff;
+    xrow[s] = g * LY::RS + xoff;
   }
+  float bsum[NS];  // per-lane partial bias sums (rows 16*to+i), reduced once at the end
+#pragma unroll
+  for (int s = 0; s < NS; ++s) bsum[s] = 0.f;
   // ---- staging: the records of the next sub-chunk are prefetched into registers
   // (branch-free, PER float4 per thread) while the current one is consumed ----
-  constexpr int R4 = RC::LEN / 4, D4 = RC::DLEN / 4, W4 = R4 + D4;
+  // A sub-chunk's records are one contiguous block of DW_NPTS * STRIDE floats: item k
+  // of this thread is float4 (threadIdx.x + k * DW_THREADS) of the block.
+  constexpr int W4 = RC::STRIDE / 4;
   constexpr int ITEMS = DW_NPTS * W4;
   constexpr int PER = (ITEMS + DW_THREADS - 1) / DW_THREADS;
   const int64_t nsub = (ctx.P + DW_NPTS - 1) / DW_NPTS;
+  const float4* recs = reinterpret_cast<const float4*>(ctx.rec + job.rec_off);
+  int dst[PER];  // LDS destination of item k (fixed for the whole kernel)
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = threadIdx.x + k * DW_THREADS;
+    const int r = e / W4, c = e - r * W4;
+    dst[k] = e < ITEMS ? r * LY::RS + LY::REC0 + 4 * c : -1;
+  }
+  // the next sub-chunk's records are prefetched into registers while the current
+  // one is consumed
   float4 pre[PER];
   auto prefetch = [&](int64_t sub) {
+    const float4* blk = recs + sub * DW_NPTS * W4;
+    const int64_t lim = (ctx.P - sub * DW_NPTS) * W4;  // valid float4s in this block
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int e = threadIdx.x + k * DW_THREADS;
-      const int ee = e < ITEMS ? e : ITEMS - 1;
-      const int r = ee / W4, c = ee - r * W4;
-      int64_t p = sub * DW_NPTS + r;
-      p = p < ctx.P ? p : ctx.P - 1;
-      const float* src = c < R4 ? ctx.rec + job.rec_off + p * RC::LEN + 4 * c
-                                : ctx.drec + job.drec_off + p * RC::DLEN + 4 * (c - R4);
-      pre[k] = *reinterpret_cast<const float4*>(src);
+      pre[k] = (e < ITEMS && e < lim) ? blk[e] : float4{0.f, 0.f, 0.f, 0.f};
     }
   };
   if (blockIdx.x < nsub) prefetch(blockIdx.x);
@@ -622,14 +647,8 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
     __syncthreads();  // previous sub-chunk's reads are done
     const int64_t p0 = sub * DW_NPTS;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = threadIdx.x + k * DW_THREADS;
-      if (e < ITEMS) {
-        const int r = e / W4, c = e - r * W4;
-        const float4 v = (p0 + r < ctx.P) ? pre[k] : float4{0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<float4*>(buf + r * LY::RS + 4 * c) = v;
-      }
-    }
+    for (int k = 0; k < PER; ++k)
+      if (dst[k] >= 0) *reinterpret_cast<float4*>(buf + dst[k]) = pre[k];
     if (threadIdx.x < 2 * DW_NPTS) {  // p.float() and d out columns
       const int r = threadIdx.x >> 1;
       const int64_t p = p0 + r;
@@ -647,36 +666,54 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
       }
     }
     __syncthreads();
+    if constexpr (N::XYZ) {  // Fourier features, exactly as wave_forward computes them
+      // (rows past P hold p = 0 and padded B columns are 0: sin(0) = 0, no checks)
+      const float* B = lds + LY::FB;
+      for (int e = threadIdx.x; e < DW_NPTS * EMBP; e += DW_THREADS) {
+        const int r = e / EMBP, m = e - r * EMBP;
+        const float4 f = *reinterpret_cast<const float4*>(buf + r * LY::RS + LY::PF);
+        buf[r * LY::RS + LY::EMB + m] =
+            NC_SIN(__builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m])));
+      }
+    }
+    // dZ_L = dh_L * relu'(Z_L) (mask bit 8L+j of lane-group g's word; L = 4: hi word)
+    for (int e = threadIdx.x; e < DW_NPTS * 40; e += DW_THREADS) {
+      const int r = e / 40, c4 = e - r * 40, L = c4 >> 3, jj = c4 & 7;
+      float* row = buf + r * LY::RS;
+      const float4 dh = *reinterpret_cast<const float4*>(row + LY::DREC + RC::DH + HID * L + 4 * jj);
+      const unsigned w = __float_as_uint(row[LY::M + 2 * (jj & 3) + (L == 4 ? 1 : 0)]) >>
+                         ((L == 4 ? 0 : 8 * L) + 4 * (jj >> 2));
+      *reinterpret_cast<float4*>(row + LY::DZ + HID * L + 4 * jj) =
+          float4{(w & 1u) ? dh.x : 0.f, (w & 2u) ? dh.y : 0.f, (w & 4u) ? dh.z : 0.f, (w & 8u) ? dh.w : 0.f};
+    }
+    __syncthreads();
     if (sub + gridDim.x < nsub) prefetch(sub + gridDim.x);
-    // ---- tiles: 8 MFMA k-steps of 4 points each ----
+    // ---- tiles: DW_NPTS/4 k-steps of 4 points; the wave's NS accumulation chains are
+    // interleaved (k-step outer) so no MFMA waits on its predecessor's result ----
+    // one k-step = NS independent MFMAs + 2 NS reads at immediate offsets; unrolled by
+    // 4 with a scheduling barrier per k-step (fully unrolled, the scheduler hoists
+    // every k-step's reads and spills)
+#pragma unroll 4
+    for (int q = 0; q < DW_NPTS / 4; ++q) {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int tau = wv + DW_WAVES * s;
-      if (tau >= TL::NT) continue;  // wave-uniform (scalar) branch
-      floatx4 a = acc[s];
-      float bs = 0.f;
-      // opaque copies: keeps LICM from hoisting 3 x 8 LDS addresses per tile out of
-      // the sub-chunk loop (which spills)
-      unsigned dyx_s = dyx[s], dm_s = dm[s];
-      asm volatile("" : "+v"(dyx_s), "+v"(dm_s));
-      const float* yrow = buf + g * LY::RS + (dyx_s & 0xffffu);
-      const float* xrow = buf + g * LY::RS + (dyx_s >> 16);
-      const float* mrow = buf + g * LY::RS + (dm_s & 0xffffu);
-      const unsigned mbit = 1u << (dm_s >> 16);
+      for (int s = 0; s < NS; ++s) {
+        const float av = buf[yrow[s] + 4 * q * LY::RS];
+        acc[s] = mfma4(av, buf[xrow[s] + 4 * q * LY::RS], acc[s]);
+        bsum[s] += av;
+      }
+    }
+  }
+  // bias gradients: each (phase, row block) is owned by its ti == 0 tile
 #pragma unroll
-      for (int q = 0; q < DW_NPTS / 4; ++q) {
-        const float y = yrow[4 * q * LY::RS];
-        const float av = (__float_as_uint(mrow[4 * q * LY::RS]) & mbit) ? y : 0.f;
-        a = mfma4(av, xrow[4 * q * LY::RS], a);
-        bs += av;
-      }
-      acc[s] = a;
-      int ph, to, ti;
-      TL::get(tau, ph, to, ti);
-      if (ti == 0 && ph <= 10) {  // wave-uniform
-        bs = sum_groups(bs);
-        if (g == 0) atomicAdd(bacc + (ph == 0 ? 0 : 16 + 32 * (ph - 1)) + 16 * to + i, bs);
-      }
+  for (int s = 0; s < NS; ++s) {
+    const int tau = wv + DW_WAVES * s;
+    if (tau >= TL::NT) continue;
+    int ph, to, ti;
+    TL::get(tau, ph, to, ti);
+    if (ti == 0 && ph <= 10) {
+      const float bs = sum_groups(bsum[s]);
+      if (g == 0) bacc[(ph == 0 ? 0 : 16 + 32 * (ph - 1)) + 16 * to + i] = bs;
     }
   }
   // ---- flush: every weight-gradient element is owned by exactly one lane and
@@ -721,7 +758,8 @@ __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int FWD_LDS_FLOATS =
-    cmax(cmax(Net<K_COARSE>::WEIGHTS, Net<K_MID>::WEIGHTS), cmax(Net<K_FINE>::WEIGHTS, Net<K_COLOR>::WEIGHTS));
+    cmax(cmax(Net<K_COARSE, PADW_FWD>::WEIGHTS, Net<K_MID, PADW_FWD>::WEIGHTS),
+         cmax(Net<K_FINE, PADW_FWD>::WEIGHTS, Net<K_COLOR, PADW_FWD>::WEIGHTS));
 constexpr int DW_LDS_FLOATS = cmax(cmax(DwLayout<K_COARSE>::TOTAL, DwLayout<K_MID>::TOTAL),
                                    cmax(DwLayout<K_FINE>::TOTAL, DwLayout<K_COLOR>::TOTAL));
 static_assert(FWD_LDS_FLOATS * 4 <= 160 * 1024, "weight image LDS budget");
@@ -733,22 +771,15 @@ int64_t max_param_count() {
   return cmax(cmax((int)Net<K_COARSE>::NPARAM, (int)Net<K_MID>::NPARAM),
               cmax((int)Net<K_FINE>::NPARAM, (int)Net<K_COLOR>::NPARAM));
 }
-int rec_len(int kind) {
+int rec_stride(int kind) {
   switch (kind) {
-    case K_COARSE: return Rec<K_COARSE>::LEN;
-    case K_MID: return Rec<K_MID>::LEN;
-    case K_FINE: return Rec<K_FINE>::LEN;
-    default: return Rec<K_COLOR>::LEN;
+    case K_COARSE: return Rec<K_COARSE>::STRIDE;
+    case K_MID: return Rec<K_MID>::STRIDE;
+    case K_FINE: return Rec<K_FINE>::STRIDE;
+    default: return Rec<K_COLOR>::STRIDE;
   }
 }
-int drec_len(int kind) {
-  switch (kind) {
-    case K_COARSE: return Rec<K_COARSE>::DLEN;
-    case K_MID: return Rec<K_MID>::DLEN;
-    case K_FINE: return Rec<K_FINE>::DLEN;
-    default: return Rec<K_COLOR>::DLEN;
-  }
-}
+
 
 template <typename K>
 static int set_lds(K kernel, int bytes) {
