@@ -1,8 +1,8 @@
 // nc_abi.hip — extern "C" entry points of libnicecore.so (see include/nicecore.h).
 //
 // Plans the launches of one render_batch_ray forward / backward:
-//   forward : [k_depth_max] -> k_ray_setup -> k_mlp_fwd (all decoders of the
-//             stage in one launch) -> k_composite_fwd
+//   forward : [k_depth_max] -> k_ray_setup -> k_grid_gather -> k_mlp_fwd (all
+//             decoders of the stage in one launch) -> k_composite_fwd
 //   backward: k_composite_bwd -> k_mlp_dx -> k_grid_bwd -> [k_mlp_dw -> k_param_reduce]
 //             -> [k_ray_grads]
 // Everything is enqueued on the caller's stream; no host synchronisation, no
@@ -36,12 +36,12 @@ int check_hip(int e, const char* what) {
 enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
-  KID_COUNT
+  KID_GRID_GATHER, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
-                                       "k_mlp_dw"};
+                                       "k_mlp_dw", "k_grid_gather"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -144,7 +144,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, rec = 0, total = 0;
+  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, rec = 0, feat = 0, total = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
   int slab_wgs = 1;
@@ -177,6 +177,13 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
       r += P * rec_stride(pl.jobs[j].kind);
     }
     w.rec = take((size_t)r * 4);
+  } else {  // forward only: features go to their own buffer
+    int64_t f = 0;
+    for (int j = 0; j < pl.n_jobs; ++j) {
+      w.rec_off[j] = f;
+      f += P * (pl.jobs[j].kind == K_FINE ? 64 : 32);
+    }
+    w.feat = take((size_t)f * 4);
   }
   const int64_t blocks = (P + 31) / 32;  // k_mlp_dw sub-chunks
   // one wave of resident workgroups over all jobs (floor: a 257th workgroup on a
@@ -205,14 +212,23 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.save_rec = w.save;
   for (int j = 0; j < pl.n_jobs; ++j) {
     m.jobs[j] = pl.jobs[j];
-    m.jobs[j].rec_off = w.rec_off[j];
     const int k = pl.jobs[j].kind;
+    m.jobs[j].rec_off = w.rec_off[j];
+    if (w.save) {
+      m.jobs[j].c_off = w.rec_off[j] + rec_feat_offset(k);
+      m.jobs[j].c_stride = rec_stride(k);
+    } else {
+      m.jobs[j].c_off = w.rec_off[j];
+      m.jobs[j].c_stride = k == K_FINE ? 64 : 32;
+    }
     m.jobs[j].need_dw = dec[k].grad != nullptr;
     m.jobs[j].need_grid = grids[k].grad != nullptr;
     m.jobs[j].need_coord = need_coord;
   }
   std::memcpy(m.grids, grids, sizeof(m.grids));
   std::memcpy(m.dec, dec, sizeof(m.dec));
+  m.share_mid = pl.n_jobs >= 2 && pl.jobs[0].kind == K_FINE && pl.jobs[1].kind == K_MID &&
+                std::memcmp(dec[K_FINE].bound, dec[K_MID].bound, sizeof(dec[K_FINE].bound)) == 0;
   m.pts = pts;
   m.xyz = at<float4>(ws, w.xyz);
   m.pf = at<float4>(ws, w.pf);
@@ -224,6 +240,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.dcbuf = at<float>(ws, w.dcbuf);
   m.slab = at<float>(ws, w.slab);
   m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
+  m.cfeat = w.save ? m.rec : at<float>(ws, w.feat);
 }
 
 int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S) {
@@ -410,6 +427,7 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
+  if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(P, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
   if (int e = check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd")) return e;
   return 0;
@@ -469,6 +487,7 @@ int nc_points_forward(const nc_points_args* a, void* ws, size_t ws_bytes, void* 
   MlpCtx m;
   fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, false);
   if (int e = check_hip(launch_points_prep(m, (float4*)m.xyz, (float4*)m.pf, s), "k_points_prep")) return e;
+  if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(a->n_points, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
   return check_hip(timed(KID_POINTS_ASSEMBLE, s, [&] { return launch_points_assemble(m, a->stage, a->raw, s); }), "k_points_assemble");
 }

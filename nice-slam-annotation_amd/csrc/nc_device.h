@@ -167,6 +167,9 @@ __device__ __forceinline__ void make_corners(const nc_grid& G, const float xyz[3
 
 // Gather the 8 channels of lane-group g (C layout: channel 16*(j>>2) + 4g + (j&3))
 // and accumulate them corner by corner in the reference order (no FMA).
+// Branch-free: an out-of-bounds corner loads the (in-bounds) channel-0 cell and its
+// value is replaced by 0 (out + 0 == out), so all corners' loads can be in flight
+// together instead of one exec-masked round trip per corner.
 template <bool VEC>
 __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int g, float out[8]) {
 #pragma unroll
@@ -177,22 +180,26 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
   return;
 #endif
   const int64_t sC = G.stride[0];
+  float v[8][8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    if (!((c.inb >> k) & 1u)) continue;
-    const float* base = G.data + c.off[k];
-    float v[8];
+    const float* base = G.data + c.off[k];  // off = 0 for out-of-bounds corners
     if (VEC) {
       const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
       const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      v[k][0] = a.x; v[k][1] = a.y; v[k][2] = a.z; v[k][3] = a.w;
+      v[k][4] = b.x; v[k][5] = b.y; v[k][6] = b.z; v[k][7] = b.w;
     } else {
+      if (k == 4) __builtin_amdgcn_sched_barrier(0);  // scalar path: 4 corners x 8 loads in flight
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = base[(int64_t)feat_of(j, g) * sC];
+      for (int j = 0; j < 8; ++j) v[k][j] = base[(int64_t)feat_of(j, g) * sC];
     }
+  }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) out[j] = out[j] + v[j] * c.w[k];
+  for (int k = 0; k < 8; ++k) {
+    const bool in = (c.inb >> k) & 1u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[k][j] * c.w[k] : 0.f);
   }
 }
 

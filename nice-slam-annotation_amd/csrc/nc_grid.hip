@@ -167,6 +167,66 @@ __global__ void __launch_bounds__(256) k_grid_bwd(const MlpCtx ctx) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Forward trilinear lookups (MLP.sample_grid_feature, decoder.py:179-188, and the
+// fine decoder's no-grad grid_middle lookup, :196-202) for every (point, job), as
+// their own high-occupancy kernel so the decoder kernel reads contiguous features.
+// Thread = (point, 4-channel chunk q): chunks 0-7 sample the job's own grid, 8-15
+// (fine decoder) grid_middle -- unless the middle decoder of the same stage has the
+// same bound, whose lookup is then written to both (MlpCtx::share_mid).  Corners and weights are make_corners (bit-identical
+// to ATen's grid_sampler_3d); channels accumulate corner by corner without FMA.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_grid_gather(const MlpCtx ctx) {
+  const unsigned y = blockIdx.y;
+  const Job job = y == 0 ? ctx.jobs[0] : (y == 1 ? ctx.jobs[1] : ctx.jobs[2]);
+  const int lg = (job.kind == K_FINE && !ctx.share_mid) ? 4 : 3;  // log2(chunks per point)
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = t >> lg;
+  if (p >= ctx.P) return;
+  const int q = (int)(t & ((1 << lg) - 1));
+  const int gk = q < 8 ? job.kind : K_MID;
+  // field-wise constant-index selects (a dynamic index into the kernel-argument
+  // grid table would go through scratch)
+  nc_grid G;
+  G = gk == 0 ? ctx.grids[0] : gk == 1 ? ctx.grids[1] : gk == 2 ? ctx.grids[2] : ctx.grids[3];
+  const float4 n = ctx.xyz[(int64_t)job.slot * ctx.P + p];
+  const float xyz[3] = {n.x, n.y, n.z};
+  Corners co;
+  make_corners(G, xyz, co);
+  const int c0 = 4 * (q & 7);
+  const bool vec = grid_vec_ok(G);
+  const int64_t sC = G.stride[0];
+  float4 v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float* base = G.data + co.off[k] + (vec ? c0 : c0 * sC);
+    if (vec) {
+      v[k] = *reinterpret_cast<const float4*>(base);
+    } else {
+      v[k] = float4{base[0], base[sC], base[2 * sC], base[3 * sC]};
+    }
+  }
+  float4 o = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool in = (co.inb >> k) & 1u;
+    const float w = co.w[k];
+    o.x = o.x + (in ? v[k].x * w : 0.f);
+    o.y = o.y + (in ? v[k].y * w : 0.f);
+    o.z = o.z + (in ? v[k].z * w : 0.f);
+    o.w = o.w + (in ? v[k].w * w : 0.f);
+  }
+  *reinterpret_cast<float4*>(ctx.cfeat + job.c_off + p * job.c_stride + 4 * q) = o;
+  if (ctx.share_mid && y == 1)  // the fine decoder's no-grad grid_middle lookup is this one
+    *reinterpret_cast<float4*>(ctx.cfeat + ctx.jobs[0].c_off + p * ctx.jobs[0].c_stride + 32 + 4 * q) = o;
+}
+
+int launch_grid_gather(const MlpCtx& c, hipStream_t s) {
+  const int64_t threads = c.P * 16;  // the widest job (fine: 16 chunks per point)
+  hipLaunchKernelGGL(k_grid_gather, dim3((unsigned)((threads + 255) / 256), c.n_jobs), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+
 int launch_grid_bwd(const MlpCtx& c, hipStream_t s) {
   const int64_t ntiles = (c.P + 15) / 16;
   int64_t blocks = (ntiles + 3) / 4;

@@ -16,9 +16,9 @@ struct Job {
   int32_t need_dw;     // decoder parameter gradient
   int32_t need_grid;   // gradient into its own grid (the fine decoder's middle lookup never has one)
   int32_t need_coord;  // gradient into the sample points
-  int32_t pad;
+  int32_t c_stride;    // floats between consecutive points' features in MlpCtx::cfeat
   int64_t rec_off;     // float offset of this job's point records in MlpCtx::rec
-  int64_t pad2;
+  int64_t c_off;       // float offset of point 0's features in MlpCtx::cfeat
 };
 
 constexpr int MAX_JOBS = 3;
@@ -29,7 +29,8 @@ struct MlpCtx {
   int32_t n_jobs;
   int32_t slab_wgs;          // workgroups per job in the k_mlp_dw launch (= gridDim.x)
   int32_t save_rec;          // forward: write the activation records
-  int32_t pad;
+  int32_t share_mid;         // jobs[0] is the fine decoder and jobs[1] the middle one with the
+                             // same bound: grid_middle is gathered once for both
   Job jobs[MAX_JOBS];
   nc_grid grids[4];
   nc_decoder_params dec[4];
@@ -42,6 +43,8 @@ struct MlpCtx {
   const float* grgb;         // [P][3] d loss / d rgb
   double* dpts;              // [n_jobs][P][3] per-decoder point gradients
   float* dcbuf;              // [n_jobs][P][32] d loss / d own-grid features (k_mlp_dx -> k_grid_bwd)
+  float* cfeat;              // grid features per job (k_grid_gather -> k_mlp_fwd): the records'
+                             // feature field when saving, else a [n_jobs][P][CD] buffer
   float* rec;                // per job [P][Rec::STRIDE]: forward activations (k_mlp_fwd) followed
                              // by backward activations (k_mlp_dx); both read by k_mlp_dw
   float* slab;               // [n_jobs][slab_wgs][slab_stride] per-workgroup parameter gradients
@@ -116,9 +119,11 @@ int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dw(const MlpCtx& c, hipStream_t s);
 int launch_grid_bwd(const MlpCtx& c, hipStream_t s);
+int launch_grid_gather(const MlpCtx& c, hipStream_t s);
+int rec_feat_offset(int kind);  // float offset of the features inside a point record
 int64_t max_param_count();
 
-constexpr int FWD_THREADS = 512;  // 8 waves, 128 points per workgroup iteration
+constexpr int FWD_THREADS = 1024; // 16 waves, 256 points per workgroup iteration (one weight image per CU)
 constexpr int DX_THREADS = 512;   // 8 waves x 16 points, barrier-free
 constexpr int DW_THREADS = 1024;  // 16 waves own the dW tiles; 32-point sub-chunks
 

@@ -89,6 +89,9 @@ __device__ __forceinline__ void mm_fwd(const float* W, int qoff, const float* x,
   const float* r1 = W + (16 + i) * LD + 4 * g + 16 * qoff;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
+    // bound the weight reads in flight to one 16-column step (the scheduler would
+    // otherwise hoist a whole layer's ds_read_b128s: 8 VGPRs per step)
+    __builtin_amdgcn_sched_barrier(0);
     const float4 w0 = *reinterpret_cast<const float4*>(r0 + 16 * q);
     const float4 w1 = *reinterpret_cast<const float4*>(r1 + 16 * q);
     a0 = mfma4(w0.x, x[4 * q + 0], a0);
@@ -116,124 +119,6 @@ __device__ __forceinline__ void mm_bwd(const float* W, int ti0, const float* dz,
 
 __device__ __forceinline__ floatx4 bias4(const float* b, int g) {
   return floatx4{b[4 * g + 0], b[4 * g + 1], b[4 * g + 2], b[4 * g + 3]};
-}
-
-// ---------------------------------------------------------------------------
-// Per-wave forward of one decoder for 16 points (recomputed in backward).
-// ---------------------------------------------------------------------------
-template <int KIND>
-struct WaveRegs {
-  float emb[Net<KIND>::XYZ ? 24 : 1];  // Fourier features, C layout over 96
-  float c[Net<KIND>::CD / 4];          // grid features (fine: [fine | middle])
-  float h[5][8];                       // block outputs h_0..h_4 (C layout)
-  unsigned mask_lo, mask_hi;           // relu(Z) > 0 bits: layer L reg j -> bit 8L+j (L=4 in hi)
-  float pf[3];                         // p.float()
-};
-
-__device__ __forceinline__ bool mask_bit(unsigned lo, unsigned hi, int L, int j) {
-  return L < 4 ? ((lo >> (8 * L + j)) & 1u) : ((hi >> j) & 1u);
-}
-
-template <int KIND>
-__device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx, int slot, int64_t p,
-                                             bool valid, int i, int g, WaveRegs<KIND>& R, float out[4]) {
-  using N = Net<KIND, PADW_FWD>;
-  // grid features (decoder.py:179-188 / :196-202); coordinates normalised once per
-  // point by k_ray_setup / k_points_prep
-  float xyz[3];
-  {
-    const float4 n = valid ? ctx.xyz[(int64_t)slot * ctx.P + p] : float4{-1.f, -1.f, -1.f, 0.f};
-    xyz[0] = n.x; xyz[1] = n.y; xyz[2] = n.z;
-    const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
-    R.pf[0] = f.x; R.pf[1] = f.y; R.pf[2] = f.z;
-  }
-  const nc_grid& G = ctx.grids[KIND];
-  {
-    Corners co;
-    make_corners(G, xyz, co);
-    if (grid_vec_ok(G)) gather8<true>(G, co, g, R.c);
-    else gather8<false>(G, co, g, R.c);
-  }
-  if constexpr (KIND == K_FINE) {
-    const nc_grid& GM = ctx.grids[K_MID];
-    Corners cm;
-    make_corners(GM, xyz, cm);
-    if (grid_vec_ok(GM)) gather8<true>(GM, cm, g, R.c + 8);
-    else gather8<false>(GM, cm, g, R.c + 8);
-  }
-  // Fourier embedding: sin(p.float() @ B), K=3 summed as fma(p2,B2, fma(p1,B1, p0*B0))
-  // which is bit-identical to the CPU reference's sgemm for this shape.
-  if constexpr (N::XYZ) {
-    const float* B = lds + N::FB;
-#pragma unroll
-    for (int j = 0; j < 24; ++j) {
-      const int m = feat_of(j, g);
-      const float x = __builtin_fmaf(R.pf[2], B[2 * EMBP + m],
-                                     __builtin_fmaf(R.pf[1], B[EMBP + m], R.pf[0] * B[m]));
-      R.emb[j] = (m < EMB) ? NC_SIN(x) : 0.f;
-    }
-  }
-  R.mask_lo = 0;
-  R.mask_hi = 0;
-#pragma unroll
-  for (int L = 0; L < 5; ++L) {
-    const float* bl = lds + N::BL + L * HID;
-    floatx4 z0 = bias4(bl, g), z1 = bias4(bl + 16, g);
-    const float* W = lds + N::lin_off(L);
-    if (L == 0) {
-      if constexpr (N::XYZ) mm_fwd<6, N::LD0>(W, 0, R.emb, z0, z1, i, g);
-      else mm_fwd<2, N::LD0>(W, 0, R.c, z0, z1, i, g);
-    } else if (L == 3) {
-      if constexpr (N::XYZ) {
-        mm_fwd<6, N::LD3>(W, 0, R.emb, z0, z1, i, g);
-        mm_fwd<2, N::LD3>(W, 6, R.h[2], z0, z1, i, g);
-      } else {
-        mm_fwd<2, N::LD3>(W, 0, R.c, z0, z1, i, g);
-        mm_fwd<2, N::LD3>(W, 2, R.h[2], z0, z1, i, g);
-      }
-    } else {
-      mm_fwd<2, N::LDH>(W, 0, R.h[L > 0 ? L - 1 : 0], z0, z1, i, g);
-    }
-    float hh[8];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      hh[r] = z0[r] > 0.f ? z0[r] : 0.f;
-      hh[4 + r] = z1[r] > 0.f ? z1[r] : 0.f;
-    }
-    unsigned bits = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bits |= (hh[j] > 0.f ? 1u : 0u) << j;
-    if (L < 4) R.mask_lo |= bits << (8 * L);
-    else R.mask_hi = bits;
-    if constexpr (N::XYZ) {
-      const float* bc = lds + N::BC + L * HID;
-      floatx4 f0, f1;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        f0[r] = hh[r] + bc[4 * g + r];
-        f1[r] = hh[4 + r] + bc[16 + 4 * g + r];
-      }
-      mm_fwd<N::CD / 16, N::LDC>(lds + N::WC + L * HID * N::LDC, 0, R.c, f0, f1, i, g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        R.h[L][r] = f0[r];
-        R.h[L][4 + r] = f1[r];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) R.h[L][j] = hh[j];
-    }
-  }
-  // output_linear (VALU dot over the point's four lanes)
-#pragma unroll
-  for (int o = 0; o < 4; ++o) {
-    if (o >= (KIND == K_COLOR ? 3 : 1)) { out[o] = 0.f; continue; }
-    const float* wo = lds + N::WO + o * HID;
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s = s + wo[feat_of(j, g)] * R.h[4][j];
-    out[o] = sum_groups(s) + lds[N::BO + o];
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -266,13 +151,124 @@ __device__ __forceinline__ void store_rows(float* dst, const float* v, int g) {
     *reinterpret_cast<float4*>(dst + 16 * t + 4 * g) = float4{v[4 * t + 0], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
 }
 
+
+// ---------------------------------------------------------------------------
+// Per-wave forward of one decoder for 16 points (recomputed in backward).
+// ---------------------------------------------------------------------------
 template <int KIND>
-__device__ __forceinline__ void save_record(float* r, const WaveRegs<KIND>& R, int g) {
-  using RC = Rec<KIND>;
+struct WaveRegs {
+  float emb[Net<KIND>::XYZ ? 24 : 1];  // Fourier features, C layout over 96
+  float c[Net<KIND>::CD / 4];          // grid features (fine: [fine | middle])
+  float h[8];                          // current block output h_L (C layout); h_4 at the end
+  float h2[8];                         // h_2, the skip input of block 3
+  unsigned mask_lo, mask_hi;           // relu(Z) > 0 bits: layer L reg j -> bit 8L+j (L=4 in hi)
+  float pf[3];                         // p.float()
+};
+
+__device__ __forceinline__ bool mask_bit(unsigned lo, unsigned hi, int L, int j) {
+  return L < 4 ? ((lo >> (8 * L + j)) & 1u) : ((hi >> j) & 1u);
+}
+
+template <int KIND>
+__device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx, int slot, int64_t p,
+                                             bool valid, int i, int g, WaveRegs<KIND>& R, float out[4],
+                                             float* rec, int64_t job_c_off, int job_c_stride) {
+  // rec != nullptr: the point's activation record (Rec<KIND>) is written as each
+  // piece is produced, so no block output stays live longer than the MLP needs it
+  using N = Net<KIND, PADW_FWD>;
+  {
+    const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
+    R.pf[0] = f.x; R.pf[1] = f.y; R.pf[2] = f.z;
+  }
+  // grid features (decoder.py:179-188 / :196-202), interpolated by k_grid_gather
+  {
+    const float* cf = ctx.cfeat + job_c_off + (valid ? p : 0) * job_c_stride + 4 * g;
 #pragma unroll
-  for (int L = 0; L < 5; ++L) store_rows<2>(r + RC::H + HID * L, R.h[L], g);
-  store_rows<Net<KIND>::CD / 16>(r + RC::C, R.c, g);
-  *reinterpret_cast<uint2*>(r + RC::M + 2 * g) = uint2{R.mask_lo, R.mask_hi};
+    for (int t = 0; t < N::CD / 16; ++t) {
+      const float4 v = valid ? *reinterpret_cast<const float4*>(cf + 16 * t) : float4{0.f, 0.f, 0.f, 0.f};
+      R.c[4 * t + 0] = v.x; R.c[4 * t + 1] = v.y; R.c[4 * t + 2] = v.z; R.c[4 * t + 3] = v.w;
+    }
+  }
+  // (the record's feature field was written by k_grid_gather)
+  // Fourier embedding: sin(p.float() @ B), K=3 summed as fma(p2,B2, fma(p1,B1, p0*B0))
+  // which is bit-identical to the CPU reference's sgemm for this shape.
+  if constexpr (N::XYZ) {
+    const float* B = lds + N::FB;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      const int m = feat_of(j, g);
+      const float x = __builtin_fmaf(R.pf[2], B[2 * EMBP + m],
+                                     __builtin_fmaf(R.pf[1], B[EMBP + m], R.pf[0] * B[m]));
+      R.emb[j] = (m < EMB) ? NC_SIN(x) : 0.f;
+    }
+  }
+  R.mask_lo = 0;
+  R.mask_hi = 0;
+#pragma unroll
+  for (int L = 0; L < 5; ++L) {
+    const float* bl = lds + N::BL + L * HID;
+    floatx4 z0 = bias4(bl, g), z1 = bias4(bl + 16, g);
+    const float* W = lds + N::lin_off(L);
+    if (L == 0) {
+      if constexpr (N::XYZ) mm_fwd<6, N::LD0>(W, 0, R.emb, z0, z1, i, g);
+      else mm_fwd<2, N::LD0>(W, 0, R.c, z0, z1, i, g);
+    } else if (L == 3) {
+      if constexpr (N::XYZ) {
+        mm_fwd<6, N::LD3>(W, 0, R.emb, z0, z1, i, g);
+        mm_fwd<2, N::LD3>(W, 6, R.h2, z0, z1, i, g);
+      } else {
+        mm_fwd<2, N::LD3>(W, 0, R.c, z0, z1, i, g);
+        mm_fwd<2, N::LD3>(W, 2, R.h2, z0, z1, i, g);
+      }
+    } else {
+      mm_fwd<2, N::LDH>(W, 0, R.h, z0, z1, i, g);
+    }
+    float hh[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      hh[r] = z0[r] > 0.f ? z0[r] : 0.f;
+      hh[4 + r] = z1[r] > 0.f ? z1[r] : 0.f;
+    }
+    unsigned bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bits |= (hh[j] > 0.f ? 1u : 0u) << j;
+    if (L < 4) R.mask_lo |= bits << (8 * L);
+    else R.mask_hi = bits;
+    if constexpr (N::XYZ) {
+      const float* bc = lds + N::BC + L * HID;
+      floatx4 f0, f1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        f0[r] = hh[r] + bc[4 * g + r];
+        f1[r] = hh[4 + r] + bc[16 + 4 * g + r];
+      }
+      mm_fwd<N::CD / 16, N::LDC>(lds + N::WC + L * HID * N::LDC, 0, R.c, f0, f1, i, g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        R.h[r] = f0[r];
+        R.h[4 + r] = f1[r];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) R.h[j] = hh[j];
+    }
+    if (L == 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) R.h2[j] = R.h[j];
+    }
+    if (rec) store_rows<2>(rec + Rec<KIND>::H + HID * L, R.h, g);
+  }
+  if (rec) *reinterpret_cast<uint2*>(rec + Rec<KIND>::M + 2 * g) = uint2{R.mask_lo, R.mask_hi};
+  // output_linear (VALU dot over the point's four lanes)
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    if (o >= (KIND == K_COLOR ? 3 : 1)) { out[o] = 0.f; continue; }
+    const float* wo = lds + N::WO + o * HID;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s = s + wo[feat_of(j, g)] * R.h[j];
+    out[o] = sum_groups(s) + lds[N::BO + o];
+  }
 }
 
 // Constant-index select: a dynamic index into the by-value kernel-argument block
@@ -299,8 +295,8 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     const bool valid = p < ctx.P;
     WaveRegs<KIND> R;
     float out[4];
-    wave_forward<KIND>(lds, ctx, job.slot, p, valid, i, g, R, out);
-    if (ctx.save_rec && valid) save_record<KIND>(ctx.rec + job.rec_off + p * Rec<KIND>::STRIDE, R, g);
+    float* rec = (ctx.save_rec && valid) ? ctx.rec + job.rec_off + p * Rec<KIND>::STRIDE : nullptr;
+    wave_forward<KIND>(lds, ctx, job.slot, p, valid, i, g, R, out, rec, job.c_off, job.c_stride);
     if (valid && g == 0) {
       if constexpr (KIND == K_COLOR) {
         ctx.rgb[p * 3 + 0] = out[0];
@@ -771,6 +767,15 @@ int64_t max_param_count() {
   return cmax(cmax((int)Net<K_COARSE>::NPARAM, (int)Net<K_MID>::NPARAM),
               cmax((int)Net<K_FINE>::NPARAM, (int)Net<K_COLOR>::NPARAM));
 }
+int rec_feat_offset(int kind) {
+  switch (kind) {
+    case K_COARSE: return Rec<K_COARSE>::C;
+    case K_MID: return Rec<K_MID>::C;
+    case K_FINE: return Rec<K_FINE>::C;
+    default: return Rec<K_COLOR>::C;
+  }
+}
+
 int rec_stride(int kind) {
   switch (kind) {
     case K_COARSE: return Rec<K_COARSE>::STRIDE;

@@ -110,7 +110,7 @@ def check(rc: int, what: str):
 KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_fwd": 3,
               "k_composite_bwd": 4, "k_mlp_dx": 5, "k_param_reduce": 6, "k_ray_grads": 7,
               "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10,
-              "k_grid_bwd": 11, "k_mlp_dw": 12}
+              "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13}
 
 
 class KernelTimer:
