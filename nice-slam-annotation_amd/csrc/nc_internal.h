@@ -124,7 +124,7 @@ int rec_feat_offset(int kind);  // float offset of the features inside a point r
 int64_t max_param_count();
 
 constexpr int FWD_THREADS = 1024; // 16 waves, 256 points per workgroup iteration (one weight image per CU)
-constexpr int DX_THREADS = 512;   // 8 waves x 16 points, barrier-free
+constexpr int DX_THREADS = 768;   // 12 waves x 16 points, barrier-free; 3 waves/SIMD at <= 170 VGPRs
 constexpr int DW_THREADS = 1024;  // 16 waves own the dW tiles; 32-point sub-chunks
 
 }  // namespace nc

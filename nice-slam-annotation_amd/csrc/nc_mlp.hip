@@ -111,6 +111,7 @@ __device__ __forceinline__ void mm_bwd(const float* W, int ti0, const float* dz,
                                        int g) {
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
+    __builtin_amdgcn_sched_barrier(0);  // bound the weight reads in flight (register pressure)
     const float* row = W + feat_of(s, g) * LD + 16 * ti0 + i;
 #pragma unroll
     for (int t = 0; t < NT; ++t) out[t] = mfma4(row[16 * t], dz[s], out[t]);
@@ -430,24 +431,28 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
     }
     float dpf[3] = {0.f, 0.f, 0.f};
     if constexpr (N::XYZ) {
+      // dx = d emb * cos(p.float() @ B), produced 4 features at a time: stored for
+      // k_mlp_dw and reduced into d p.float() = B dx without keeping all 24 live
       const float* B = lds + N::FB;
       const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
-      float dx[24];
 #pragma unroll
-      for (int j = 0; j < 24; ++j) {
-        const int m = feat_of(j, g);
-        const float x = __builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m]));
-        dx[j] = (m < EMB) ? demb[j >> 2][j & 3] * NC_COS(x) : 0.f;
+      for (int t = 0; t < 6; ++t) {
+        float dx4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * t + 4 * g + r;
+          const float x = __builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m]));
+          dx4[r] = (m < EMB) ? demb[t][r] * NC_COS(x) : 0.f;
+          dpf[0] = dpf[0] + B[m] * dx4[r];
+          dpf[1] = dpf[1] + B[EMBP + m] * dx4[r];
+          dpf[2] = dpf[2] + B[2 * EMBP + m] * dx4[r];
+        }
+        if (need_dw && valid)
+          *reinterpret_cast<float4*>(drec + RC::DX + 16 * t + 4 * g) = float4{dx4[0], dx4[1], dx4[2], dx4[3]};
       }
-      if (need_dw && valid) store_rows<6>(drec + RC::DX, dx, g);
       if (need_coord) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          float s = 0.f;
-#pragma unroll
-          for (int j = 0; j < 24; ++j) s = s + B[k * EMBP + feat_of(j, g)] * dx[j];
-          dpf[k] = sum_groups(s);
-        }
+        for (int k = 0; k < 3; ++k) dpf[k] = sum_groups(dpf[k]);
       }
     }
     if (need_dc && valid) {

@@ -282,6 +282,7 @@ class NiceRenderFn(torch.autograd.Function):
         device = rays_o.device
         if device.type != "cuda":
             raise L.NiceCoreError("nicecore renders on a HIP device; tensors are on " + str(device))
+        ctx.set_materialize_grads(False)  # unused outputs: NULL upstream gradient, no zero fill
         rays_o = rays_o.detach().float().contiguous()
         rays_d = rays_d.detach().float().contiguous()
         N = rays_o.shape[0]
