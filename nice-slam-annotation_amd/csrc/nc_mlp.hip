@@ -89,9 +89,6 @@ __device__ __forceinline__ void mm_fwd(const float* W, int qoff, const float* x,
   const float* r1 = W + (16 + i) * LD + 4 * g + 16 * qoff;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    // bound the weight reads in flight to one 16-column step (the scheduler would
-    // otherwise hoist a whole layer's ds_read_b128s: 8 VGPRs per step)
-    __builtin_amdgcn_sched_barrier(0);
     const float4 w0 = *reinterpret_cast<const float4*>(r0 + 16 * q);
     const float4 w1 = *reinterpret_cast<const float4*>(r1 + 16 * q);
     a0 = mfma4(w0.x, x[4 * q + 0], a0);
@@ -111,7 +108,6 @@ __device__ __forceinline__ void mm_bwd(const float* W, int ti0, const float* dz,
                                        int g) {
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    __builtin_amdgcn_sched_barrier(0);  // bound the weight reads in flight (register pressure)
     const float* row = W + feat_of(s, g) * LD + 16 * ti0 + i;
 #pragma unroll
     for (int t = 0; t < NT; ++t) out[t] = mfma4(row[16 * t], dz[s], out[t]);

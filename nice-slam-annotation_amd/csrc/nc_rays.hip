@@ -297,18 +297,42 @@ __global__ void __launch_bounds__(256) k_ray_grads(const RayCtx c) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_param_reduce(const ParamReduceCtx c) {
+// thread = (float4 column of the parameter vector, part): part p sums slab rows
+// p, p+8, ... (independent loads in flight), the 8 partial sums meet in LDS.
+constexpr int PR_COLS = 32, PR_PARTS = 8;
+__global__ void __launch_bounds__(PR_COLS * PR_PARTS) k_param_reduce(const ParamReduceCtx c) {
+  __shared__ float4 part[PR_PARTS][PR_COLS];
   const int j = blockIdx.y;
   // constant-index selects (dynamic indexing of the argument block spills it)
   const Job job = j == 0 ? c.jobs[0] : (j == 1 ? c.jobs[1] : c.jobs[2]);
   float* grad = j == 0 ? c.grad[0] : (j == 1 ? c.grad[1] : c.grad[2]);
   const int64_t np = j == 0 ? c.nparam[0] : (j == 1 ? c.nparam[1] : c.nparam[2]);
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (!job.need_dw || grad == nullptr || e >= np) return;
-  const float* src = c.slab + (int64_t)j * c.slab_wgs * c.slab_stride + e;
-  float s = 0.f;
-  for (int w = 0; w < c.slab_wgs; ++w) s += src[(int64_t)w * c.slab_stride];
-  grad[e] = s;
+  if (!job.need_dw || grad == nullptr) return;
+  const int col = threadIdx.x % PR_COLS, prt = threadIdx.x / PR_COLS;
+  const int64_t e = ((int64_t)blockIdx.x * PR_COLS + col) * 4;  // first parameter of the column
+  if ((int64_t)blockIdx.x * PR_COLS * 4 >= np) return;          // whole workgroup past the end
+  float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+  if (e < c.slab_stride) {  // slab rows are padded to slab_stride (multiple of 64 floats)
+    const float* src = c.slab + (int64_t)j * c.slab_wgs * c.slab_stride + e;
+    for (int w = prt; w < c.slab_wgs; w += PR_PARTS) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)w * c.slab_stride);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  part[prt][col] = acc;
+  __syncthreads();
+  if (prt == 0) {
+    float4 s4 = part[0][col];
+#pragma unroll
+    for (int q = 1; q < PR_PARTS; ++q) {
+      const float4 v = part[q][col];
+      s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+    }
+    const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (e + k < np) grad[e + k] = sv[k];
+  }
 }
 
 // ---- NICE.forward on caller points (decoder.py:336-370) ----
@@ -372,8 +396,8 @@ int launch_ray_grads(const RayCtx& c, hipStream_t s) {
   return (int)hipGetLastError();
 }
 int launch_param_reduce(const ParamReduceCtx& c, int64_t max_nparam, hipStream_t s) {
-  dim3 grid((unsigned)((max_nparam + 255) / 256), c.n_jobs);
-  hipLaunchKernelGGL(k_param_reduce, grid, dim3(256), 0, s, c);
+  dim3 grid((unsigned)((max_nparam + 4 * PR_COLS - 1) / (4 * PR_COLS)), c.n_jobs);
+  hipLaunchKernelGGL(k_param_reduce, grid, dim3(PR_COLS * PR_PARTS), 0, s, c);
   return (int)hipGetLastError();
 }
 int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s) {
