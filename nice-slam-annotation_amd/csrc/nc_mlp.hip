@@ -220,15 +220,19 @@ __device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx
     } else {
       mm_fwd<2, N::LDH>(W, 0, R.h, z0, z1, i, g);
     }
+    // relu and its mask from one compare per value (no IEEE-canonicalising max pair)
     float hh[8];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      hh[r] = z0[r] > 0.f ? z0[r] : 0.f;
-      hh[4 + r] = z1[r] > 0.f ? z1[r] : 0.f;
-    }
     unsigned bits = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bits |= (hh[j] > 0.f ? 1u : 0u) << j;
+    for (int r = 0; r < 4; ++r) {
+      const bool p0 = z0[r] > 0.f, p1 = z1[r] > 0.f;
+      hh[r] = p0 ? z0[r] : 0.f;
+      hh[4 + r] = p1 ? z1[r] : 0.f;
+#ifndef NC_ABL_NO_MASK  // timing-only ablation: no relu mask bits
+      bits |= (p0 ? 1u : 0u) << r;
+      bits |= (p1 ? 1u : 0u) << (4 + r);
+#endif
+    }
     if (L < 4) R.mask_lo |= bits << (8 * L);
     else R.mask_hi = bits;
     if constexpr (N::XYZ) {
@@ -292,7 +296,11 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     const bool valid = p < ctx.P;
     WaveRegs<KIND> R;
     float out[4];
+#ifdef NC_ABL_NO_RECSTORE  // timing-only ablation: the forward writes no activation record
+    float* rec = nullptr;
+#else
     float* rec = (ctx.save_rec && valid) ? ctx.rec + job.rec_off + p * Rec<KIND>::STRIDE : nullptr;
+#endif
     wave_forward<KIND>(lds, ctx, job.slot, p, valid, i, g, R, out, rec, job.c_off, job.c_stride);
     if (valid && g == 0) {
       if constexpr (KIND == K_COLOR) {

@@ -40,12 +40,15 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, extra=()) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, extra=(), out: str | None = None) -> str:
+    """Compile libnicecore.so (or, with ``out``, a variant library at that path --
+    timing ablations, tools/ablate.py)."""
+    lib = out or LIB
+    if out is None and not force and not needs_build():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-           "-I", INCLUDE, "-I", CSRC, *extra, "-o", LIB + ".tmp",
+           "-I", INCLUDE, "-I", CSRC, *extra, "-o", lib + ".tmp",
            *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -54,8 +57,8 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> str:
         raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
     if verbose and (r.stdout or r.stderr):
         print(r.stdout + r.stderr)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":

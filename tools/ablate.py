@@ -1,0 +1,47 @@
+"""Timing ablations of the render core: build variant libraries (compile-time
+NC_ABL_* switches that remove one piece of work; results are WRONG, timing only)
+and print the per-kernel breakdown of the C2 bench step for each.
+
+    python tools/ablate.py build            # in the build container (hipcc)
+    python tools/ablate.py run [variants]   # on the GPU box
+"""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "nice-slam-annotation_amd"))
+DBG = os.path.join(REPO, "dbg")
+VARIANTS = {
+    "base": [],
+    "no_trig": ["-DNC_ABL_NO_TRIG"],
+    "no_recstore": ["-DNC_ABL_NO_RECSTORE"],
+    "no_mask": ["-DNC_ABL_NO_MASK"],
+}
+# variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
+
+if __name__ == "__main__":
+    cmd = sys.argv[1]
+    names = sys.argv[2:] or list(VARIANTS)
+    if cmd == "build":
+        from nicecore import build as B
+        os.makedirs(DBG, exist_ok=True)
+        for n in names:
+            print(B.build(force=True, extra=VARIANTS[n], out=os.path.join(DBG, f"abl_{n}.so")), flush=True)
+    else:
+        for n in names:
+            if not os.path.exists(os.path.join(DBG, f"abl_{n}.so")):
+                print(n, "missing", flush=True)
+                continue
+            env = dict(os.environ, NICECORE_LIB=os.path.join(DBG, f"abl_{n}.so"))
+            r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "3",
+                                "--cpu-seconds", "0"], env=env, capture_output=True, text=True, timeout=300)
+            line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            if r.returncode != 0 or not line:
+                print(n, "FAILED", r.returncode, r.stderr[-2000:], flush=True)
+                break
+            import json
+            d = json.loads(line[-1])
+            ks = d["kernels_ms"]
+            print(f"{n:14s} step {d['ms_per_step']:.4f} ms  " +
+                  "  ".join(f"{k.replace('k_', '')} {v * 1e3:.1f}" for k, v in ks.items()), flush=True)
