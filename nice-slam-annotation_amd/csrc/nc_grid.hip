@@ -75,7 +75,8 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
     OFF[i * 8 + 2 * g + 1] = base + G.grad_stride[3];
   }
   if (g == 0) {
-    KEY[i] = valid ? ((c.z0 * G.dims[1] + c.y0) * G.dims[2] + c.x0) : -1;
+    // cell coordinates packed into the key (x | y << 21 | z << 42; grids < 2^21 per axis)
+    KEY[i] = valid ? (c.x0 | (c.y0 << 21) | (c.z0 << 42)) : -1;
     INB[i] = valid ? (int)c.inb : 0;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -86,31 +87,60 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
   float acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  // Walk the half's 8 samples in order.  acc[k] holds corner k of the current cell.
+  // Same cell: keep accumulating.  Next cell one step away along one axis: the 4
+  // corners of the shared face carry over, the other 4 are flushed.  Otherwise all
+  // 8 are flushed.  One atomic instruction = one 128-B corner row (lane = channel).
   int run = half * 8;
   int64_t cur = KEY[run];
-  auto flush = [&](int pt) {
-    const int inb = INB[pt];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if ((inb >> k) & 1) {
-        atomicAdd(G.grad + OFF[pt * 8 + k] + chs, acc[k]);
-      }
+  auto flush_k = [&](int pt, int k) {
+    if ((INB[pt] >> k) & 1) atomicAdd(G.grad + OFF[pt * 8 + k] + chs, acc[k]);
   };
   for (int j = 0; j < 8; ++j) {
     const int pt = half * 8 + j;
     const int64_t kk = KEY[pt];
     if (kk != cur) {
-      flush(run);
+      const int64_t d = kk - cur;  // exact for one-step moves (no borrow across fields)
+      int axis = -1, dir = 0;
+      if (cur >= 0 && kk >= 0) {
+        if (d == 1) { axis = 0; dir = 1; }
+        else if (d == -1) { axis = 0; dir = -1; }
+        else if (d == (int64_t(1) << 21)) { axis = 1; dir = 1; }
+        else if (d == -(int64_t(1) << 21)) { axis = 1; dir = -1; }
+        else if (d == (int64_t(1) << 42)) { axis = 2; dir = 1; }
+        else if (d == -(int64_t(1) << 42)) { axis = 2; dir = -1; }
+      }
+      if (axis < 0) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+        for (int k = 0; k < 8; ++k) { flush_k(run, k); acc[k] = 0.f; }
+      } else {
+        // corners with the axis bit == (dir > 0 ? 1 : 0) form the shared face: they
+        // become the new cell's corners with the bit flipped
+        const int bit = 1 << axis;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const bool leaving = ((k & bit) != 0) == (dir < 0);  // face not shared
+          if (leaving) flush_k(run, k);
+        }
+        float nacc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int src = k ^ bit;  // same corner in the old cell's numbering
+          const bool from_old = ((k & bit) != 0) == (dir < 0);
+          nacc[k] = from_old ? acc[src] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = nacc[k];
+      }
       cur = kk;
     }
-    const float d = D[pt * 32 + ch];
+    const float dv = D[pt * 32 + ch];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = acc[k] + Wt[pt * 8 + k] * d;
+    for (int k = 0; k < 8; ++k) acc[k] = acc[k] + Wt[pt * 8 + k] * dv;
     run = pt;
   }
-  flush(run);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) flush_k(run, k);
 }
 
 __device__ __forceinline__ Job pick_job3(const Job (&jobs)[MAX_JOBS], unsigned y) {
