@@ -299,7 +299,7 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
 }
 
 int fwd_grid_x(int64_t P, int n_jobs, int which = 0) {
-  const int64_t per = (which == 0 ? FWD_THREADS : DX_THREADS) / 64 * 16;
+  const int64_t per = which == 0 ? FWD_THREADS / 64 * 16 * FWD_TILES : DX_THREADS / 64 * 16;
   const int64_t blocks = (P + per - 1) / per;
   int x = cu_count() * mlp_blocks_per_cu(which) / n_jobs;
   if (x < 1) x = 1;

@@ -123,6 +123,7 @@ int launch_grid_gather(const MlpCtx& c, hipStream_t s);
 int rec_feat_offset(int kind);  // float offset of the features inside a point record
 int64_t max_param_count();
 
+constexpr int FWD_TILES = 1;      // 16-point tiles per wave (2: interleaved chains, 248 VGPRs: slower)
 constexpr int FWD_THREADS = 768;  // 12 waves, 192 points per WG iteration; measured best of 512/768/1024
 constexpr int DX_THREADS = 768;   // 12 waves x 16 points, barrier-free; 3 waves/SIMD at <= 170 VGPRs
 constexpr int DW_THREADS = 1024;  // 16 waves own the dW tiles; 32-point sub-chunks

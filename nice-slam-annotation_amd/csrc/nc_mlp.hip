@@ -87,10 +87,16 @@ __device__ __forceinline__ void mm_fwd(const float* W, int qoff, const float* x,
                                        floatx4& a1, int i, int g) {
   const float* r0 = W + i * LD + 4 * g + 16 * qoff;
   const float* r1 = W + (16 + i) * LD + 4 * g + 16 * qoff;
+  // software-pipelined: step q+1's weight reads are issued before step q's MFMAs
+  float4 w0 = *reinterpret_cast<const float4*>(r0);
+  float4 w1 = *reinterpret_cast<const float4*>(r1);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const float4 w0 = *reinterpret_cast<const float4*>(r0 + 16 * q);
-    const float4 w1 = *reinterpret_cast<const float4*>(r1 + 16 * q);
+    float4 n0 = w0, n1 = w1;
+    if (q + 1 < NQ) {
+      n0 = *reinterpret_cast<const float4*>(r0 + 16 * (q + 1));
+      n1 = *reinterpret_cast<const float4*>(r1 + 16 * (q + 1));
+    }
     a0 = mfma4(w0.x, x[4 * q + 0], a0);
     a1 = mfma4(w1.x, x[4 * q + 0], a1);
     a0 = mfma4(w0.y, x[4 * q + 1], a0);
@@ -99,6 +105,38 @@ __device__ __forceinline__ void mm_fwd(const float* W, int qoff, const float* x,
     a1 = mfma4(w1.z, x[4 * q + 2], a1);
     a0 = mfma4(w0.w, x[4 * q + 3], a0);
     a1 = mfma4(w1.w, x[4 * q + 3], a1);
+    w0 = n0;
+    w1 = n1;
+  }
+}
+
+// T independent 16-point tiles through the same weights: 2T accumulation chains
+// interleaved, so one tile's dependency bubbles are filled by the other's MFMAs.
+template <int NQ, int LD, int T>
+__device__ __forceinline__ void mm_fwd_t(const float* W, int qoff, const float* (&x)[T], floatx4 (&a0)[T],
+                                         floatx4 (&a1)[T], int i, int g) {
+  const float* r0 = W + i * LD + 4 * g + 16 * qoff;
+  const float* r1 = W + (16 + i) * LD + 4 * g + 16 * qoff;
+  float4 w0 = *reinterpret_cast<const float4*>(r0);
+  float4 w1 = *reinterpret_cast<const float4*>(r1);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    float4 n0 = w0, n1 = w1;
+    if (q + 1 < NQ) {
+      n0 = *reinterpret_cast<const float4*>(r0 + 16 * (q + 1));
+      n1 = *reinterpret_cast<const float4*>(r1 + 16 * (q + 1));
+    }
+    const float wa[4] = {w0.x, w0.y, w0.z, w0.w}, wb[4] = {w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        a0[t] = mfma4(wa[k], x[t][4 * q + k], a0[t]);
+        a1[t] = mfma4(wb[k], x[t][4 * q + k], a1[t]);
+      }
+    }
+    w0 = n0;
+    w1 = n1;
   }
 }
 
@@ -166,27 +204,13 @@ __device__ __forceinline__ bool mask_bit(unsigned lo, unsigned hi, int L, int j)
   return L < 4 ? ((lo >> (8 * L + j)) & 1u) : ((hi >> j) & 1u);
 }
 
-template <int KIND>
-__device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx, int slot, int64_t p,
-                                             bool valid, int i, int g, WaveRegs<KIND>& R, float out[4],
-                                             float* rec, int64_t job_c_off, int job_c_stride) {
-  // rec != nullptr: the point's activation record (Rec<KIND>) is written as each
-  // piece is produced, so no block output stays live longer than the MLP needs it
+template <int KIND, int T>
+__device__ __forceinline__ void wave_forward(const float* lds, int i, int g, WaveRegs<KIND> (&R)[T],
+                                             float (&out)[T][4], float* const (&rec)[T]) {
+  // R[t].pf / R[t].c: the tiles' inputs (grid features of decoder.py:179-188 /
+  // :196-202, interpolated by k_grid_gather), loaded by the caller.  rec[t] != nullptr:
+  // the point's activation record (Rec<KIND>) is written as each piece is produced.
   using N = Net<KIND, PADW_FWD>;
-  {
-    const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
-    R.pf[0] = f.x; R.pf[1] = f.y; R.pf[2] = f.z;
-  }
-  // grid features (decoder.py:179-188 / :196-202), interpolated by k_grid_gather
-  {
-    const float* cf = ctx.cfeat + job_c_off + (valid ? p : 0) * job_c_stride + 4 * g;
-#pragma unroll
-    for (int t = 0; t < N::CD / 16; ++t) {
-      const float4 v = valid ? *reinterpret_cast<const float4*>(cf + 16 * t) : float4{0.f, 0.f, 0.f, 0.f};
-      R.c[4 * t + 0] = v.x; R.c[4 * t + 1] = v.y; R.c[4 * t + 2] = v.z; R.c[4 * t + 3] = v.w;
-    }
-  }
-  // (the record's feature field was written by k_grid_gather)
   // Fourier embedding: sin(p.float() @ B), K=3 summed as fma(p2,B2, fma(p1,B1, p0*B0))
   // which is bit-identical to the CPU reference's sgemm for this shape.
   if constexpr (N::XYZ) {
@@ -194,121 +218,189 @@ __device__ __forceinline__ void wave_forward(const float* lds, const MlpCtx& ctx
 #pragma unroll
     for (int j = 0; j < 24; ++j) {
       const int m = feat_of(j, g);
-      const float x = __builtin_fmaf(R.pf[2], B[2 * EMBP + m],
-                                     __builtin_fmaf(R.pf[1], B[EMBP + m], R.pf[0] * B[m]));
-      R.emb[j] = (m < EMB) ? NC_SIN(x) : 0.f;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float x = __builtin_fmaf(R[t].pf[2], B[2 * EMBP + m],
+                                       __builtin_fmaf(R[t].pf[1], B[EMBP + m], R[t].pf[0] * B[m]));
+        R[t].emb[j] = (m < EMB) ? NC_SIN(x) : 0.f;
+      }
     }
   }
-  R.mask_lo = 0;
-  R.mask_hi = 0;
+#pragma unroll
+  for (int t = 0; t < T; ++t) R[t].mask_lo = R[t].mask_hi = 0;
+  const float* xemb[T];
+  const float* xc[T];
+  const float* xh[T];
+  const float* xh2[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    xemb[t] = R[t].emb;
+    xc[t] = R[t].c;
+    xh[t] = R[t].h;
+    xh2[t] = R[t].h2;
+  }
 #pragma unroll
   for (int L = 0; L < 5; ++L) {
     const float* bl = lds + N::BL + L * HID;
-    floatx4 z0 = bias4(bl, g), z1 = bias4(bl + 16, g);
+    floatx4 z0[T], z1[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      z0[t] = bias4(bl, g);
+      z1[t] = bias4(bl + 16, g);
+    }
     const float* W = lds + N::lin_off(L);
     if (L == 0) {
-      if constexpr (N::XYZ) mm_fwd<6, N::LD0>(W, 0, R.emb, z0, z1, i, g);
-      else mm_fwd<2, N::LD0>(W, 0, R.c, z0, z1, i, g);
+      if constexpr (N::XYZ) mm_fwd_t<6, N::LD0, T>(W, 0, xemb, z0, z1, i, g);
+      else mm_fwd_t<2, N::LD0, T>(W, 0, xc, z0, z1, i, g);
     } else if (L == 3) {
       if constexpr (N::XYZ) {
-        mm_fwd<6, N::LD3>(W, 0, R.emb, z0, z1, i, g);
-        mm_fwd<2, N::LD3>(W, 6, R.h2, z0, z1, i, g);
+        mm_fwd_t<6, N::LD3, T>(W, 0, xemb, z0, z1, i, g);
+        mm_fwd_t<2, N::LD3, T>(W, 6, xh2, z0, z1, i, g);
       } else {
-        mm_fwd<2, N::LD3>(W, 0, R.c, z0, z1, i, g);
-        mm_fwd<2, N::LD3>(W, 2, R.h2, z0, z1, i, g);
+        mm_fwd_t<2, N::LD3, T>(W, 0, xc, z0, z1, i, g);
+        mm_fwd_t<2, N::LD3, T>(W, 2, xh2, z0, z1, i, g);
       }
     } else {
-      mm_fwd<2, N::LDH>(W, 0, R.h, z0, z1, i, g);
+      mm_fwd_t<2, N::LDH, T>(W, 0, xh, z0, z1, i, g);
     }
     // relu and its mask from one compare per value (no IEEE-canonicalising max pair)
-    float hh[8];
-    unsigned bits = 0;
+    floatx4 f0[T], f1[T];
+    const float* bc = lds + N::BC + L * HID;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool p0 = z0[r] > 0.f, p1 = z1[r] > 0.f;
-      hh[r] = p0 ? z0[r] : 0.f;
-      hh[4 + r] = p1 ? z1[r] : 0.f;
+    for (int t = 0; t < T; ++t) {
+      float hh[8];
+      unsigned bits = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool p0 = z0[t][r] > 0.f, p1 = z1[t][r] > 0.f;
+        hh[r] = p0 ? z0[t][r] : 0.f;
+        hh[4 + r] = p1 ? z1[t][r] : 0.f;
 #ifndef NC_ABL_NO_MASK  // timing-only ablation: no relu mask bits
-      bits |= (p0 ? 1u : 0u) << r;
-      bits |= (p1 ? 1u : 0u) << (4 + r);
+        bits |= (p0 ? 1u : 0u) << r;
+        bits |= (p1 ? 1u : 0u) << (4 + r);
 #endif
+      }
+      if (L < 4) R[t].mask_lo |= bits << (8 * L);
+      else R[t].mask_hi = bits;
+      if constexpr (N::XYZ) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f0[t][r] = hh[r] + bc[4 * g + r];
+          f1[t][r] = hh[4 + r] + bc[16 + 4 * g + r];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) R[t].h[j] = hh[j];
+      }
     }
-    if (L < 4) R.mask_lo |= bits << (8 * L);
-    else R.mask_hi = bits;
     if constexpr (N::XYZ) {
-      const float* bc = lds + N::BC + L * HID;
-      floatx4 f0, f1;
+      mm_fwd_t<N::CD / 16, N::LDC, T>(lds + N::WC + L * HID * N::LDC, 0, xc, f0, f1, i, g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        f0[r] = hh[r] + bc[4 * g + r];
-        f1[r] = hh[4 + r] + bc[16 + 4 * g + r];
-      }
-      mm_fwd<N::CD / 16, N::LDC>(lds + N::WC + L * HID * N::LDC, 0, R.c, f0, f1, i, g);
+      for (int t = 0; t < T; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        R.h[r] = f0[r];
-        R.h[4 + r] = f1[r];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) R.h[j] = hh[j];
+        for (int r = 0; r < 4; ++r) {
+          R[t].h[r] = f0[t][r];
+          R[t].h[4 + r] = f1[t][r];
+        }
     }
-    if (L == 2) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) R.h2[j] = R.h[j];
+    for (int t = 0; t < T; ++t) {
+      if (L == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) R[t].h2[j] = R[t].h[j];
+      }
+      if (rec[t]) store_rows<2>(rec[t] + Rec<KIND>::H + HID * L, R[t].h, g);
     }
-    if (rec) store_rows<2>(rec + Rec<KIND>::H + HID * L, R.h, g);
   }
-  if (rec) *reinterpret_cast<uint2*>(rec + Rec<KIND>::M + 2 * g) = uint2{R.mask_lo, R.mask_hi};
-  // output_linear (VALU dot over the point's four lanes)
 #pragma unroll
-  for (int o = 0; o < 4; ++o) {
-    if (o >= (KIND == K_COLOR ? 3 : 1)) { out[o] = 0.f; continue; }
-    const float* wo = lds + N::WO + o * HID;
-    float s = 0.f;
+  for (int t = 0; t < T; ++t) {
+    if (rec[t]) *reinterpret_cast<uint2*>(rec[t] + Rec<KIND>::M + 2 * g) = uint2{R[t].mask_lo, R[t].mask_hi};
+    // output_linear (VALU dot over the point's four lanes)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s = s + wo[feat_of(j, g)] * R.h[j];
-    out[o] = sum_groups(s) + lds[N::BO + o];
+    for (int o = 0; o < 4; ++o) {
+      if (o >= (KIND == K_COLOR ? 3 : 1)) { out[t][o] = 0.f; continue; }
+      const float* wo = lds + N::WO + o * HID;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = s + wo[feat_of(j, g)] * R[t].h[j];
+      out[t][o] = sum_groups(s) + lds[N::BO + o];
+    }
   }
-}
-
-// Constant-index select: a dynamic index into the by-value kernel-argument block
-// would make the compiler copy the whole block to scratch.
-__device__ __forceinline__ Job pick_job(const Job (&jobs)[MAX_JOBS], unsigned y) {
-  return y == 0 ? jobs[0] : (y == 1 ? jobs[1] : jobs[2]);
 }
 
 // ---------------------------------------------------------------------------
 // forward kernel
 // ---------------------------------------------------------------------------
+// Constant-index select: a dynamic index into the by-value kernel-argument block
+// (ctx.jobs[blockIdx.y]) would make the compiler copy the whole block to scratch.
+__device__ __forceinline__ Job pick_job(const Job (&jobs)[MAX_JOBS], unsigned y) {
+  return y == 0 ? jobs[0] : (y == 1 ? jobs[1] : jobs[2]);
+}
+
 template <int KIND>
 __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float* lds) {
+  constexpr int T = FWD_TILES;
+  constexpr int CQ = Net<KIND>::CD / 16;
   load_weights<KIND, PADW_FWD>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
-  const int64_t per = 16 * waves;
+  const int64_t per = 16 * waves * T;  // points per workgroup iteration
   const int64_t nblk = (ctx.P + per - 1) / per;
+  // tile t of this wave: points blk*per + (t*waves + wave)*16 + [0, 16)
+  auto point = [&](int64_t blk, int t) { return blk * per + (int64_t)(t * waves + wave) * 16 + i; };
+  // inputs of the wave's next tiles (p.float() and the grid features) are loaded one
+  // iteration ahead, so their latency hides behind the current tiles' MLP
+  float4 nf[T];
+  float4 nc[T][CQ];
+  auto load_inputs = [&](int64_t blk) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int64_t p = point(blk, t);
+      const bool ok = blk < nblk && p < ctx.P;
+      nf[t] = ok ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
+      const float* cf = ctx.cfeat + job.c_off + (ok ? p : 0) * job.c_stride + 4 * g;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q)
+        nc[t][q] = ok ? *reinterpret_cast<const float4*>(cf + 16 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_inputs(blockIdx.x);
   for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     // keep the (loop-invariant) LDS weight reads inside the loop: hoisting all of
     // them out of the persistent loop would need thousands of registers
     asm volatile("" ::: "memory");
-    const int64_t p = blk * per + wave * 16 + i;
-    const bool valid = p < ctx.P;
-    WaveRegs<KIND> R;
-    float out[4];
+    WaveRegs<KIND> R[T];
+    float* rec[T];
+    int64_t pt[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      pt[t] = point(blk, t);
+      R[t].pf[0] = nf[t].x; R[t].pf[1] = nf[t].y; R[t].pf[2] = nf[t].z;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        R[t].c[4 * q + 0] = nc[t][q].x; R[t].c[4 * q + 1] = nc[t][q].y;
+        R[t].c[4 * q + 2] = nc[t][q].z; R[t].c[4 * q + 3] = nc[t][q].w;
+      }
 #ifdef NC_ABL_NO_RECSTORE  // timing-only ablation: the forward writes no activation record
-    float* rec = nullptr;
+      rec[t] = nullptr;
 #else
-    float* rec = (ctx.save_rec && valid) ? ctx.rec + job.rec_off + p * Rec<KIND>::STRIDE : nullptr;
+      rec[t] = (ctx.save_rec && pt[t] < ctx.P) ? ctx.rec + job.rec_off + pt[t] * Rec<KIND>::STRIDE : nullptr;
 #endif
-    wave_forward<KIND>(lds, ctx, job.slot, p, valid, i, g, R, out, rec, job.c_off, job.c_stride);
-    if (valid && g == 0) {
-      if constexpr (KIND == K_COLOR) {
-        ctx.rgb[p * 3 + 0] = out[0];
-        ctx.rgb[p * 3 + 1] = out[1];
-        ctx.rgb[p * 3 + 2] = out[2];
-      } else {
-        ctx.occ[(int64_t)job.slot * ctx.P + p] = out[0];
+    }
+    load_inputs(blk + gridDim.x);
+    float out[T][4];
+    wave_forward<KIND, T>(lds, i, g, R, out, rec);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int64_t p = pt[t];
+      if (p < ctx.P && g == 0) {
+        if constexpr (KIND == K_COLOR) {
+          ctx.rgb[p * 3 + 0] = out[t][0];
+          ctx.rgb[p * 3 + 1] = out[t][1];
+          ctx.rgb[p * 3 + 2] = out[t][2];
+        } else {
+          ctx.occ[(int64_t)job.slot * ctx.P + p] = out[t][0];
+        }
       }
     }
   }

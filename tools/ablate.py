@@ -17,6 +17,11 @@ VARIANTS = {
     "no_trig": ["-DNC_ABL_NO_TRIG"],
     "no_recstore": ["-DNC_ABL_NO_RECSTORE"],
     "no_mask": ["-DNC_ABL_NO_MASK"],
+    "dw_no_emb": ["-DNC_ABL_DW_NO_EMB"],
+    "dw_no_maskpass": ["-DNC_ABL_DW_NO_MASKPASS"],
+    "dw_no_stage": ["-DNC_ABL_DW_NO_STAGE"],
+    "dw_no_load": ["-DNC_ABL_DW_NO_LOAD"],
+    "dw_no_mfma": ["-DNC_ABL_DW_NO_MFMA"],
 }
 # variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
 
