@@ -107,6 +107,7 @@ def make_step(w, args, world, device):
     step and the graph-replayed step (render + loss + backward captured once into a
     hipGraph, nicecore.graph.GraphedStep; the collectives stay outside the graph)."""
     import torch.distributed as dist
+    from nicecore import distributed as ND
     grids, model, renderer = w["grids"], w["model"], w["renderer"]
     ro, rd, gt, gtc = w["ro"], w["rd"], w["gt"], w["gtc"]
     params = [p for p in model.parameters() if p.requires_grad]
@@ -132,10 +133,8 @@ def make_step(w, args, world, device):
         return loss
 
     def post():
-        if world > 1 and w["ba"]:
-            hs = [dist.all_reduce(t.grad, async_op=True) for t in gvals + params if t.grad is not None]
-            for h in hs:
-                h.wait()
+        if world > 1 and w["ba"]:  # one RCCL SUM over the core's shared gradient buffer
+            ND.allreduce_grads(gvals + params)
 
     def eager():
         pre()

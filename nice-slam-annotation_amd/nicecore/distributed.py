@@ -41,17 +41,39 @@ def global_depth_max(gt_depth: torch.Tensor, group=None) -> torch.Tensor:
     return m
 
 
+def _shared_bases(grads):
+    """Split grads into (buffers reduced whole, remaining grads): a base tensor whose
+    elements are exactly covered by views in ``grads`` (the render core puts every
+    gradient of one backward call into one buffer: render_fn._alloc_grads) is
+    reduced once instead of per view."""
+    by_base = {}
+    for g in grads:
+        b = g._base
+        if b is not None and b.is_contiguous():
+            by_base.setdefault(id(b), (b, []))[1].append(g)
+    whole, covered = [], set()
+    for b, views in by_base.values():
+        if sum(v.numel() for v in views) == b.numel() and all(v.dtype == b.dtype for v in views):
+            whole.append(b)
+            covered.update(id(v) for v in views)
+    return whole, [g for g in grads if id(g) not in covered]
+
+
 def allreduce_grads(tensors, group=None, bucket_bytes: int = 4 << 20):
     """SUM all-reduce of the ``.grad`` of every tensor that has one.
 
-    Gradients larger than ``bucket_bytes`` are reduced in place (async, overlapped);
-    the small ones are packed into flat buckets, reduced, and unpacked."""
+    Buffers fully covered by the gradients (the render core's single gradient
+    buffer per backward call) are reduced with one collective each.  Remaining
+    gradients larger than ``bucket_bytes`` are reduced in place (async); the small
+    ones are packed into flat buckets, reduced, and unpacked."""
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):
         return
     grads = [t.grad for t in tensors if t.grad is not None]
+    whole, grads = _shared_bases(grads)
+    handles = [dist.all_reduce(b, group=group, async_op=True) for b in whole]
     big = [g for g in grads if g.numel() * g.element_size() >= bucket_bytes]
     small = [g for g in grads if g.numel() * g.element_size() < bucket_bytes]
-    handles = [dist.all_reduce(g, group=group, async_op=True) for g in big]
+    handles += [dist.all_reduce(g, group=group, async_op=True) for g in big]
     by_dtype = {}
     for g in small:
         by_dtype.setdefault((g.dtype, g.device), []).append(g)

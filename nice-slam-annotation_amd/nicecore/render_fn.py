@@ -240,18 +240,43 @@ class _Plan:
 _PLANS = weakref.WeakKeyDictionary()  # decoders module -> {stage: _Plan}
 
 
-def _alloc_param_grads(lib, plan, needs_params, args, device):
-    """flat gradient buffers (one per decoder whose params need grad)."""
-    flats = {}
+def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device):
+    """Every gradient of one backward call lives in ONE float32 buffer: the grid
+    gradients first (strided views with each grid's own memory format, zero-filled
+    by a single kernel), then one flat parameter vector per decoder whose
+    parameters need a gradient (written, not accumulated, by the library).  The
+    views are stolen by AccumulateGrad as the leaves' .grad (their strides obey
+    the layout contract), and distributed.allreduce_grads reduces the shared
+    buffer with one collective."""
     sl = plan.param_slices()
+    gk = [k for k in plan.grids if needs_grids[k]]
+    pk = [k for k in plan.decs if any(needs_params[sl[k][0]:sl[k][1]])]
+    gsize = sum(grids[k].numel() for k in gk)
+    psize = {k: int(lib.nc_param_count(k)) for k in pk}
+    buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
+    if gsize:
+        buf[:gsize].zero_()
+    grid_grads = [None] * 4
+    off = 0
+    for k in plan.grids:
+        args.grids[k].grad = None
+    for k in gk:
+        g = grids[k]
+        gg = torch.as_strided(buf, g.shape, g.stride(), off)
+        args.grids[k].grad = gg.data_ptr()
+        st = gg.stride()
+        for ax in range(4):
+            args.grids[k].grad_stride[ax] = st[1 + ax]
+        grid_grads[k] = gg
+        off += g.numel()
+    flats = {}
     for k in plan.decs:
-        a, b = sl[k]
-        if any(needs_params[a:b]):
-            flats[k] = torch.empty(lib.nc_param_count(k), device=device, dtype=torch.float32)
-            args.dec[k].grad = flats[k].data_ptr()
-        else:
-            args.dec[k].grad = None
-    return flats
+        args.dec[k].grad = None
+    for k in pk:
+        flats[k] = buf[off:off + psize[k]]
+        args.dec[k].grad = flats[k].data_ptr()
+        off += psize[k]
+    return grid_grads, flats
 
 
 def _split_param_grads(plan, flats, needs_params):
@@ -341,18 +366,8 @@ class NiceRenderFn(torch.autograd.Function):
             g_ro = g_ro if g_ro is not None else torch.empty_like(rays_o)
             g_rd = g_rd if g_rd is not None else torch.empty_like(rays_o)
         a.g_rays_o, a.g_rays_d = _ptr(g_ro), _ptr(g_rd)
-        grid_grads = [None] * 4
-        for k in plan.grids:
-            a.grids[k].grad = None
-            if need[4 + k]:
-                gg = torch.zeros_like(ctx.grids[k])  # keeps the grid's memory format
-                st = gg.stride()
-                a.grids[k].grad = gg.data_ptr()
-                for ax in range(4):
-                    a.grids[k].grad_stride[ax] = st[1 + ax]
-                grid_grads[k] = gg
         needs_params = need[8:]
-        flats = _alloc_param_grads(lib, plan, needs_params, a, device)
+        grid_grads, flats = _alloc_grads(lib, plan, needs_params, need[4:8], ctx.grids, a, device)
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_render_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
                 "nc_render_backward")
@@ -407,18 +422,8 @@ class NiceEvalFn(torch.autograd.Function):
         a.g_raw = gr.data_ptr()
         g_pts = torch.empty_like(pts) if need[1] else None
         a.g_pts = _ptr(g_pts)
-        grid_grads = [None] * 4
-        for k in plan.grids:
-            a.grids[k].grad = None
-            if need[2 + k]:
-                gg = torch.zeros_like(ctx.grids[k])
-                st = gg.stride()
-                a.grids[k].grad = gg.data_ptr()
-                for ax in range(4):
-                    a.grids[k].grad_stride[ax] = st[1 + ax]
-                grid_grads[k] = gg
         needs_params = need[6:]
-        flats = _alloc_param_grads(lib, plan, needs_params, a, device)
+        grid_grads, flats = _alloc_grads(lib, plan, needs_params, need[2:6], ctx.grids, a, device)
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_points_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
                 "nc_points_backward")

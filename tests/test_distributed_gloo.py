@@ -110,3 +110,50 @@ def test_local_depth_max_changes_outputs():
     torch.testing.assert_close(glob, full[a:b], rtol=0, atol=0)
     if float(dep.max()) != float(rec["gt_depth"].max()):
         assert float((local - full[a:b]).abs().max()) > 0
+
+
+def _shared_buffer_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import conftest  # noqa: F401  (paths)
+    from nicecore import distributed as ND
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # leaves whose .grad are views of ONE buffer (as render_fn._alloc_grads makes them,
+    # grid-like strided view included) plus one ordinary gradient
+    buf = torch.arange(40, dtype=torch.float32) * (rank + 1)
+    a = torch.zeros(2, 3, requires_grad=True)
+    b = torch.zeros(1, 2, 2, 2, 2, requires_grad=True)   # 16 elements
+    c = torch.zeros(18, requires_grad=True)
+    d = torch.zeros(5, requires_grad=True)
+    a.grad = buf[0:6].view(2, 3)
+    b.grad = torch.as_strided(buf, (1, 2, 2, 2, 2), (16, 1, 8, 4, 2), 6)
+    c.grad = buf[22:40]
+    d.grad = torch.full((5,), float(rank + 1))
+    whole, rest = ND._shared_bases([a.grad, b.grad, c.grad, d.grad])
+    n_whole = len(whole)
+    ND.allreduce_grads([a, b, c, d])
+    if rank == 0:
+        out.put((n_whole, len(rest), buf.numpy().copy(), d.grad.numpy().copy(), a.grad.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_shared_gradient_buffer():
+    """One collective over a buffer the gradients fully cover; values are summed."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shared_buffer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    n_whole, n_rest, buf, dgrad, agrad = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert n_whole == 1 and n_rest == 1
+    np.testing.assert_array_equal(buf, np.arange(40, dtype=np.float32) * 3)   # 1x + 2x
+    np.testing.assert_array_equal(dgrad, np.full(5, 3.0, dtype=np.float32))
+    np.testing.assert_array_equal(agrad, buf[0:6].reshape(2, 3))
