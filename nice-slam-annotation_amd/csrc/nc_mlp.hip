@@ -159,11 +159,11 @@ __device__ __forceinline__ floatx4 bias4(const float* b, int g) {
 // ---------------------------------------------------------------------------
 // Per-point activation record saved by the forward for the backward kernels
 // (float offsets; every block starts on a 16-byte boundary):
-//   [h_0..h_4 5x32] [c CD] [relu masks: lane-group g -> u32 lo, hi]
+//   [h_0..h_4 5x32] [c CD] [relu masks: lane-group g -> u32 lo, hi] [p.float(), 0]
 // The Fourier features are not stored: k_mlp_dw recomputes them from p.float()
 // with the forward's own fourier_sin (bit-identical, ~110 MB less traffic a step).
 // Backward record written by k_mlp_dx right after it (same point, offset LEN):
-// [dh_0..dh_4 5x32] [dx 96 (xyz)] where dh_L is
+// [dh_0..dh_4 5x32] [dx 96 (xyz)] [d out, 0-padded to 4] where dh_L is
 // d loss / d h_L (block L's output) and dx = d loss / d (p @ B).
 // ---------------------------------------------------------------------------
 template <int KIND>
@@ -172,11 +172,14 @@ struct Rec {
   static constexpr int H = 0;
   static constexpr int C = H + 5 * HID;
   static constexpr int M = C + N::CD;
-  static constexpr int LEN = M + 8;
+  static constexpr int PF = M + 8;           // p.float() (x, y, z, 0)
+  static constexpr int LEN = PF + 4;
   static constexpr int DH = 0;
   static constexpr int DX = 5 * HID;
-  static constexpr int DLEN = DX + (N::XYZ ? EMBP : 0);
+  static constexpr int DOUT = DX + (N::XYZ ? EMBP : 0);  // d loss / d output (4; unused rows 0)
+  static constexpr int DLEN = DOUT + 4;
   static constexpr int STRIDE = LEN + DLEN;  // one point: [forward record | backward record]
+  static_assert(STRIDE % 32 == 16, "record stride must be 16 mod 32 (k_mlp_dw operand banks)");
 };
 
 template <int NT>
@@ -314,7 +317,10 @@ __device__ __forceinline__ void wave_forward(const float* lds, int i, int g, Wav
   }
 #pragma unroll
   for (int t = 0; t < T; ++t) {
-    if (rec[t]) *reinterpret_cast<uint2*>(rec[t] + Rec<KIND>::M + 2 * g) = uint2{R[t].mask_lo, R[t].mask_hi};
+    if (rec[t]) {
+      *reinterpret_cast<uint2*>(rec[t] + Rec<KIND>::M + 2 * g) = uint2{R[t].mask_lo, R[t].mask_hi};
+      if (g == 0) *reinterpret_cast<float4*>(rec[t] + Rec<KIND>::PF) = float4{R[t].pf[0], R[t].pf[1], R[t].pf[2], 0.f};
+    }
     // output_linear (VALU dot over the point's four lanes)
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
@@ -481,6 +487,8 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
       const uint2 m = *reinterpret_cast<const uint2*>(rec + RC::M + 2 * g);
       mlo = m.x;
       mhi = m.y;
+      if (need_dw && g == 0)  // k_mlp_dw reads d out from the record
+        *reinterpret_cast<float4*>(drec + RC::DOUT) = float4{dout[0], dout[1], dout[2], 0.f};
     }
     float dh[8];
 #pragma unroll
@@ -591,16 +599,16 @@ constexpr int DW_NPTS = 32;  // points per staged sub-chunk (8 MFMA k-steps)
 template <int KIND>
 struct DwLayout {
   using RC = Rec<KIND>;
-  // row: [emb 96 (xyz decoders, recomputed)] [forward record] [backward record] [pf] [d out]
+  // row: [emb 96 (xyz decoders, recomputed)] [forward record] [backward record] [dZ]
   static constexpr int EMB = 0;
   static constexpr int REC0 = Net<KIND>::XYZ ? EMBP : 0;
   static constexpr int H = REC0 + RC::H;
   static constexpr int C = REC0 + RC::C;
   static constexpr int M = REC0 + RC::M;
   static constexpr int DREC = REC0 + RC::LEN;    // backward record follows the forward one
-  static constexpr int PF = DREC + RC::DLEN;     // p.float() (4)
-  static constexpr int DOUT = PF + 4;            // d out (4; rows >= NOUT zero)
-  static constexpr int DZ = DOUT + 4;            // dZ_L = dh_L * relu'(Z_L), 5 x 32 (staged)
+  static constexpr int PF = REC0 + RC::PF;       // p.float() (4)
+  static constexpr int DOUT = DREC + RC::DOUT;   // d out (4; rows >= NOUT zero)
+  static constexpr int DZ = DREC + RC::DLEN;     // dZ_L = dh_L * relu'(Z_L), 5 x 32 (staged)
   static constexpr int RS = DZ + 5 * HID;        // row stride (== 16 mod 32)
   static constexpr int BUF = DW_NPTS * RS;
   static constexpr int BACC = BUF;               // bias accumulators after the buffer
@@ -746,22 +754,6 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (dst[k] >= 0) *reinterpret_cast<float4*>(buf + dst[k]) = pre[k];
-    if (threadIdx.x < 2 * DW_NPTS) {  // p.float() and d out columns
-      const int r = threadIdx.x >> 1;
-      const int64_t p = p0 + r;
-      float4 v = float4{0.f, 0.f, 0.f, 0.f};
-      if (threadIdx.x & 1) {
-        if (p < ctx.P) {
-          if constexpr (KIND == K_COLOR) v = float4{ctx.grgb[p * 3 + 0], ctx.grgb[p * 3 + 1], ctx.grgb[p * 3 + 2], 0.f};
-          else v.x = ctx.gocc[p];
-        }
-        *reinterpret_cast<float4*>(buf + r * LY::RS + LY::DOUT) = v;
-      } else {
-        if (p < ctx.P) v = ctx.pf[p];
-        v.w = __uint_as_float(0xffffffffu);  // all-ones mask slot
-        *reinterpret_cast<float4*>(buf + r * LY::RS + LY::PF) = v;
-      }
-    }
     __syncthreads();
     if constexpr (N::XYZ) {  // Fourier features, exactly as wave_forward computes them
       // (rows past P hold p = 0 and padded B columns are 0: sin(0) = 0, no checks)
