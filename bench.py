@@ -167,6 +167,24 @@ def algorithmic_flops_per_ray(stage, S, mode):
     return {"k_mlp_fwd": fwd * S, "k_mlp_dx": dx * S, "k_mlp_dw": dw * S}
 
 
+# point-record geometry of the core (csrc/nc_mlp.hip Rec<KIND>): floats per point
+REC_STRIDE = {"coarse": 368, "middle": 464, "fine": 496, "color": 464}
+REC_LEN = {"coarse": 204, "middle": 204, "fine": 236, "color": 204}
+FEAT = {"coarse": 32, "middle": 32, "fine": 64, "color": 32}
+NOUT = {"coarse": 1, "middle": 1, "fine": 1, "color": 3}
+
+
+def algorithmic_bytes_per_point(stage, mode):
+    """HBM bytes a kernel must move per sample point: its inputs and
+    outputs, the saved activation records included (they are the backward's input)."""
+    decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
+            "color": ["fine", "middle", "color"]}[stage]
+    fwd = sum(4 * FEAT[d] + 16 + 4 * (REC_LEN[d] - FEAT[d]) + 4 * NOUT[d] for d in decs)
+    dx = sum(32 + 4 * NOUT[d] + 16 + 4 * (REC_STRIDE[d] - REC_LEN[d]) + 128 + 24 for d in decs)
+    dw = sum(4 * REC_STRIDE[d] for d in decs) if mode == "ba" else 0
+    return {"k_mlp_fwd": fwd, "k_mlp_dx": dx, "k_mlp_dw": dw}
+
+
 def cpu_baseline(args, seconds):
     """The CPU oracle (torch-CPU restatement of the reference path) on a bounded sample."""
     from oracle import nice_oracle as O
@@ -289,16 +307,28 @@ def main():
 
     S = 48
     per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode)
+    per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode)
     fl = per_ray[dominant] * args.rays if dominant in per_ray else None
+    by = per_pt_bytes[dominant] * args.rays * S if dominant in per_pt_bytes else None
     roof = None
-    if fl is not None and avg_ms > 0:
-        ach = fl / (avg_ms * 1e-3) / 1e12
+    if fl is not None and by and avg_ms > 0:
+        tflops = fl / (avg_ms * 1e-3) / 1e12
+        gbs = by / (avg_ms * 1e-3) / 1e9
         tr = read_traffic()
-        roof = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 3),
-                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes"), "avg_launch_ms": round(avg_ms, 4),
-                "flop_per_launch": fl, "timing": timing_src}
+        traffic = ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes")
+        ridge = FP32_MFMA_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # FLOP per byte
+        hbm_bound = fl / by < ridge
+        roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dominant,
+                "achieved": round(gbs if hbm_bound else tflops, 3),
+                "peak": HBM_PEAK_GBS if hbm_bound else FP32_MFMA_PEAK_TFLOPS,
+                "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
+                "flop_per_launch": fl, "bytes_per_launch": by,
+                "intensity_flop_per_byte": round(fl / by, 2), "ridge_flop_per_byte": round(ridge, 2),
+                "mfma_tflops": round(tflops, 3), "mfma_frac": round(tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+                "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                "timing": timing_src}
 
     value = world * args.rays * args.steps / dt
     out = {
