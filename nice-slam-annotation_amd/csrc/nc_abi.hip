@@ -3,8 +3,8 @@
 // Plans the launches of one render_batch_ray forward / backward:
 //   forward : [k_depth_max] -> k_ray_setup -> k_grid_gather -> k_mlp_fwd (all
 //             decoders of the stage in one launch) -> k_composite_fwd
-//   backward: k_composite_bwd -> k_mlp_dx -> k_grid_bwd -> [k_mlp_dw -> k_param_reduce]
-//             -> [k_ray_grads]
+//   backward: k_composite_bwd -> k_mlp_dx (incl. the trilinear backward) ->
+//             [k_mlp_dw -> k_param_reduce] -> [k_ray_grads]
 // Everything is enqueued on the caller's stream; no host synchronisation, no
 // device allocation (graph-capturable).
 #include <hip/hip_runtime.h>
@@ -144,7 +144,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, dcbuf = 0, slab = 0, rec = 0, feat = 0, total = 0;
+  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0, total = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
   int slab_wgs = 1;
@@ -168,7 +168,6 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
   w.gocc = take((size_t)P * 4);
   w.grgb = take((size_t)P * 12);
   w.dpts = take((size_t)pl.n_jobs * P * 24);
-  w.dcbuf = take((size_t)pl.n_jobs * P * 32 * 4);
   w.save = save;
   if (save) {
     int64_t r = 0;
@@ -237,7 +236,6 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.gocc = at<float>(ws, w.gocc);
   m.grgb = at<float>(ws, w.grgb);
   m.dpts = at<double>(ws, w.dpts);
-  m.dcbuf = at<float>(ws, w.dcbuf);
   m.slab = at<float>(ws, w.slab);
   m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
   m.cfeat = w.save ? m.rec : at<float>(ws, w.feat);
@@ -319,12 +317,11 @@ int64_t nparam_of(int kind) {
 
 int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s);
 
-// decoder backward: dX chains (+ d features, Fourier point gradient) -> trilinear
-// backward -> weight gradients -> slab reduction
+// decoder backward: dX chains + trilinear backward (k_mlp_dx) -> weight gradients
+// -> slab reduction
 int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s) {
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
   if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs, 1), s); }), "k_mlp_dx")) return e;
-  if (int e = check_hip(timed(KID_GRID_BWD, s, [&] { return launch_grid_bwd(m, s); }), "k_grid_bwd")) return e;
   bool any_dw = false;
   for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;
   if (any_dw)

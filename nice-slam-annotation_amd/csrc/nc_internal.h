@@ -42,7 +42,6 @@ struct MlpCtx {
   const float* gocc;         // [P] d loss / d occupancy (shared by the occupancy decoders)
   const float* grgb;         // [P][3] d loss / d rgb
   double* dpts;              // [n_jobs][P][3] per-decoder point gradients
-  float* dcbuf;              // [n_jobs][P][32] d loss / d own-grid features (k_mlp_dx -> k_grid_bwd)
   float* cfeat;              // grid features per job (k_grid_gather -> k_mlp_fwd): the records'
                              // feature field when saving, else a [n_jobs][P][CD] buffer
   float* rec;                // per job [P][Rec::STRIDE]: forward activations (k_mlp_fwd) followed
@@ -113,12 +112,12 @@ int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s);
 
 int mlp_fwd_lds_bytes();
 int mlp_dw_lds_bytes();
+int mlp_dx_lds_bytes();
 int mlp_blocks_per_cu(int which);  // 0 k_mlp_fwd, 1 k_mlp_dx, 2 k_mlp_dw
 int rec_stride(int kind);  // floats per point of a decoder's [forward | backward] record
 int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dw(const MlpCtx& c, hipStream_t s);
-int launch_grid_bwd(const MlpCtx& c, hipStream_t s);
 int launch_grid_gather(const MlpCtx& c, hipStream_t s);
 int rec_feat_offset(int kind);  // float offset of the features inside a point record
 int64_t max_param_count();

@@ -25,6 +25,7 @@
 //     flushed once into an LDS image of the flat parameter vector and written
 //     to a per-workgroup slab (reduced by nc_rays.hip:k_param_reduce).
 #include "nc_device.h"
+#include "nc_grid.h"
 #include "nc_internal.h"
 
 #ifdef NC_ABL_NO_TRIG  // timing-only ablation: no trig at all
@@ -456,12 +457,21 @@ struct PhaseMap {
 // dx = d emb ⊙ cos(p @ B); d p.float() = B dx.  Writes dh_L and dx for k_mlp_dw,
 // d features for k_grid_bwd and the Fourier part of the point gradient.
 // ---------------------------------------------------------------------------
+__host__ __device__ constexpr int cmax_(int a, int b) { return a > b ? a : b; }
+// k_mlp_dx LDS: its weight image, then one grid-scatter slice per wave
+constexpr int DX_SLICE_BASE = cmax_(cmax_(Net<K_COARSE, PADW_BWD>::WEIGHTS, Net<K_MID, PADW_BWD>::WEIGHTS),
+                                    cmax_(Net<K_FINE, PADW_BWD>::WEIGHTS, Net<K_COLOR, PADW_BWD>::WEIGHTS));
+static_assert(DX_SLICE_BASE % 4 == 0, "scatter slices hold int64 arrays");
+constexpr int DX_LDS_FLOATS = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
+static_assert(DX_LDS_FLOATS * 4 <= 160 * 1024, "dX LDS budget");
+
 template <int KIND>
 __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float* lds) {
   using N = Net<KIND>;
   using RC = Rec<KIND>;
   load_weights<KIND, PADW_BWD>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int waves = blockDim.x >> 6;
   const bool need_dw = job.need_dw != 0;
   const bool need_grid = job.need_grid != 0;
@@ -559,15 +569,41 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         for (int k = 0; k < 3; ++k) dpf[k] = sum_groups(dpf[k]);
       }
     }
-    if (need_dc && valid) {
-      float* dst = ctx.dcbuf + ((int64_t)job.slot * ctx.P + p) * HID;
-      *reinterpret_cast<float4*>(dst + 4 * g) = float4{dc[0][0], dc[0][1], dc[0][2], dc[0][3]};
-      *reinterpret_cast<float4*>(dst + 16 + 4 * g) = float4{dc[1][0], dc[1][1], dc[1][2], dc[1][3]};
+    // trilinear backward of this decoder's own grid lookup (nc_grid.h): coordinate
+    // gradient and grid scatter, fused here so the scatter's atomics overlap other
+    // waves' MFMA work
+    double gg[3] = {0.0, 0.0, 0.0};
+    if (need_dc) {
+      const nc_grid& G = ctx.grids[KIND];
+      const float4 n = valid ? ctx.xyz[(int64_t)job.slot * ctx.P + p] : float4{-1.f, -1.f, -1.f, 0.f};
+      const float xyz[3] = {n.x, n.y, n.z};
+      Corners co;
+      make_corners(G, xyz, co);
+      float dcv[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dcv[r] = valid ? dc[0][r] : 0.f;
+        dcv[4 + r] = valid ? dc[1][r] : 0.f;
+      }
+      if (need_coord) {
+        float gi[3];
+        if (grid_vec_ok(G)) grid_coord_grad<true>(G, co, dcv, g, gi);
+        else grid_coord_grad<false>(G, co, dcv, g, gi);
+        const float gm[3] = {co.gmx, co.gmy, co.gmz};
+        const nc_decoder_params& D = ctx.dec[KIND];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          // normalize_3d_coordinate backward: (g * 2) / (hi - lo)
+          const float gk = sum_groups(gi[k]) * gm[k];
+          gg[k] = ((double)gk * 2.0) / (D.bound[k][1] - D.bound[k][0]);
+        }
+      }
+      if (need_grid) grid_scatter(G, co, dcv, valid, slice, i, g, lane);
     }
     if (need_coord && valid && g == 0) {
       double* dst = ctx.dpts + ((int64_t)job.slot * ctx.P + p) * 3;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) dst[k] = (double)dpf[k];
+      for (int k = 0; k < 3; ++k) dst[k] = gg[k] + (double)dpf[k];
     }
   }
 }
@@ -897,8 +933,8 @@ int mlp_blocks_per_cu(int which) {
       set_lds(k_mlp_fwd, mlp_fwd_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd, FWD_THREADS, mlp_fwd_lds_bytes());
     } else if (which == 1) {
-      set_lds(k_mlp_dx, mlp_fwd_lds_bytes());
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dx, DX_THREADS, mlp_fwd_lds_bytes());
+      set_lds(k_mlp_dx, mlp_dx_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dx, DX_THREADS, mlp_dx_lds_bytes());
     } else {
       set_lds(k_mlp_dw, mlp_dw_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dw, DW_THREADS, mlp_dw_lds_bytes());
@@ -915,10 +951,12 @@ int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+int mlp_dx_lds_bytes() { return DX_LDS_FLOATS * 4; }
+
 int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s) {
   static int attr = -1;
-  if (attr != 0 && (attr = set_lds(k_mlp_dx, mlp_fwd_lds_bytes())) != 0) return attr;
-  hipLaunchKernelGGL(k_mlp_dx, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_fwd_lds_bytes(), s, c);
+  if (attr != 0 && (attr = set_lds(k_mlp_dx, mlp_dx_lds_bytes())) != 0) return attr;
+  hipLaunchKernelGGL(k_mlp_dx, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 
