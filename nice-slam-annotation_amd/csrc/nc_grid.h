@@ -14,29 +14,39 @@ namespace nc {
 template <bool VEC>
 __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners& c, const float dc[8], int g,
                                                 float gi[3]) {
+  // branch-free in two batches of 4 corners (all 4 corners' loads in flight; an
+  // out-of-bounds corner reads the in-bounds cell 0 and contributes 0), corner
+  // order and association as the reference
   gi[0] = gi[1] = gi[2] = 0.f;
   const int64_t sC = G.stride[0];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (!((c.inb >> k) & 1u)) continue;
-    const int xb = k & 1, yb = (k >> 1) & 1, zb = k >> 2;
-    const float* base = G.data + c.off[k];
-    float v[8];
-    if (VEC) {
-      const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
-      const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    } else {
+  for (int h = 0; h < 2; ++h) {
+    float v[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = base[(int64_t)feat_of(j, g) * sC];
+    for (int kk = 0; kk < 4; ++kk) {
+      const float* base = G.data + c.off[4 * h + kk];
+      if (VEC) {
+        const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
+        const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
+        v[kk][0] = a.x; v[kk][1] = a.y; v[kk][2] = a.z; v[kk][3] = a.w;
+        v[kk][4] = b.x; v[kk][5] = b.y; v[kk][6] = b.z; v[kk][7] = b.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[kk][j] = base[(int64_t)feat_of(j, g) * sC];
+      }
     }
-    float dot = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dot = dot + v[j] * dc[j];
-    gi[0] = gi[0] + (xb ? dot : -dot) * c.wy[yb] * c.wz[zb];
-    gi[1] = gi[1] + (yb ? dot : -dot) * c.wx[xb] * c.wz[zb];
-    gi[2] = gi[2] + (zb ? dot : -dot) * c.wx[xb] * c.wy[yb];
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * h + kk;
+      if (!((c.inb >> k) & 1u)) continue;  // out-of-bounds corner: no contribution
+      const int xb = k & 1, yb = (k >> 1) & 1, zb = k >> 2;
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot = dot + v[kk][j] * dc[j];
+      gi[0] = gi[0] + (xb ? dot : -dot) * c.wy[yb] * c.wz[zb];
+      gi[1] = gi[1] + (yb ? dot : -dot) * c.wx[xb] * c.wz[zb];
+      gi[2] = gi[2] + (zb ? dot : -dot) * c.wx[xb] * c.wy[yb];
+    }
   }
 }
 
