@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-oracle sample (0 disables)")
     ap.add_argument("--layout", default="channels_last", choices=["channels_last", "ncdhw"])
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse "
+                         "the multi-rank path on one GPU)")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -65,8 +68,12 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = local % torch.cuda.device_count()  # == local on a node with >= N GPUs
+        torch.cuda.set_device(dev)
+        if args.backend == "nccl":  # RCCL
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:  # rehearsal of the N>1 path with several ranks on one GPU
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, local

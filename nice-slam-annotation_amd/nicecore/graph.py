@@ -44,7 +44,9 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool):
+        # thread_local: CUDA calls of other host threads (e.g. a process group's
+        # watchdog) during the capture do not invalidate it
+        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
             self.out = _detach(body())
 
     def __call__(self):
