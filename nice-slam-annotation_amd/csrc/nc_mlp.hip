@@ -118,15 +118,21 @@ __device__ __forceinline__ void mm_fwd_t(const float* W, int qoff, const float* 
                                          floatx4 (&a1)[T], int i, int g) {
   const float* r0 = W + i * LD + 4 * g + 16 * qoff;
   const float* r1 = W + (16 + i) * LD + 4 * g + 16 * qoff;
+#ifdef NC_ABL_FWD_NOLDS  // timing-only ablation: weights never read from LDS
+  float4 w0 = float4{0.01f * i, 0.02f, 0.03f * g, 0.04f}, w1 = float4{0.05f, 0.06f * i, 0.07f, 0.08f * g};
+#else
   float4 w0 = *reinterpret_cast<const float4*>(r0);
   float4 w1 = *reinterpret_cast<const float4*>(r1);
+#endif
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     float4 n0 = w0, n1 = w1;
+#ifndef NC_ABL_FWD_NOLDS
     if (q + 1 < NQ) {
       n0 = *reinterpret_cast<const float4*>(r0 + 16 * (q + 1));
       n1 = *reinterpret_cast<const float4*>(r1 + 16 * (q + 1));
     }
+#endif
     const float wa[4] = {w0.x, w0.y, w0.z, w0.w}, wb[4] = {w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

@@ -17,6 +17,8 @@ VARIANTS = {
     "no_trig": ["-DNC_ABL_NO_TRIG"],
     "no_recstore": ["-DNC_ABL_NO_RECSTORE"],
     "no_mask": ["-DNC_ABL_NO_MASK"],
+    "fwd_nolds": ["-DNC_ABL_FWD_NOLDS"],
+    "fwd_nolds_notrig": ["-DNC_ABL_FWD_NOLDS", "-DNC_ABL_NO_TRIG", "-DNC_ABL_NO_RECSTORE"],
     "dw_no_emb": ["-DNC_ABL_DW_NO_EMB"],
     "dw_no_maskpass": ["-DNC_ABL_DW_NO_MASKPASS"],
     "dw_no_stage": ["-DNC_ABL_DW_NO_STAGE"],
