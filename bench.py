@@ -108,9 +108,17 @@ def build_workload(args, rank, device):
     return w
 
 
+# the callers' loss configuration (configs/nice_slam.yaml: mapping.w_color_loss 0.2,
+# tracking.w_color_loss 0.5, use_color_in_tracking, handle_dynamic)
+LOSS_KW = {
+    "ba": lambda stage: dict(loss="mapper", w_color_loss=0.2, color_term=stage == "color"),
+    "tracker": lambda stage: dict(loss="tracker", w_color_loss=0.5, color_term=True, handle_dynamic=True),
+}
+
+
 def make_step(w, args, world, device):
-    """One iteration = [all-reduce(MAX) of the depth bound] -> render_batch_ray ->
-    Mapper L1 loss -> backward -> [all-reduce of the gradients].  Returns the eager
+    """One iteration = [all-reduce(MAX) of the depth bound] -> render_batch_ray with the
+    fused Mapper (BA) / Tracker loss -> backward -> [all-reduce of the gradients].  Returns the eager
     step and the graph-replayed step (render + loss + backward captured once into a
     hipGraph, nicecore.graph.GraphedStep; the collectives stay outside the graph)."""
     import torch.distributed as dist
@@ -119,8 +127,8 @@ def make_step(w, args, world, device):
     ro, rd, gt, gtc = w["ro"], w["rd"], w["gt"], w["gtc"]
     params = [p for p in model.parameters() if p.requires_grad]
     gvals = [g for g in grids.values() if g.requires_grad]
-    depth_mask = (gt > 0).double()
     dmax = gt.max().reshape(1).clone() if world > 1 else None  # static buffer
+    loss_kw = LOSS_KW[args.mode](args.stage)
 
     def pre():
         if world > 1:  # Renderer.py:157/:194 use max(gt_depth) over the whole (sharded) batch
@@ -130,12 +138,10 @@ def make_step(w, args, world, device):
     def body():
         for t in params + gvals + [ro, rd]:
             t.grad = None
-        depth, unc, color = renderer.render_batch_ray(grids, model, rd, ro, device, args.stage,
-                                                      gt, depth_max=dmax)
-        # src/Mapper.py:603-612 (mask applied multiplicatively: same gradient, no host sync)
-        loss = ((gt.double() - depth).abs() * depth_mask).sum()
-        if args.stage == "color":
-            loss = loss + 0.2 * (gtc - color).abs().sum()
+        # render_batch_ray + the caller's loss in the same launches (k_loss):
+        # Mapper.py:603-612 (BA mode) / Tracker.py:117-131 (tracker mode)
+        depth, unc, color, loss = renderer.render_batch_loss(
+            grids, model, rd, ro, device, args.stage, gt, gtc, **loss_kw, depth_max=dmax)
         loss.backward()
         return loss
 
@@ -206,7 +212,7 @@ def cpu_baseline(args, seconds):
     g = {k: v.requires_grad_(args.mode == "ba") for k, v in grids.items()}
     dec_b = S.decoder_bounds(sc.bound)
     ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000)
-    mask = (dep > 0).double()
+    kw = LOSS_KW[args.mode](args.stage)
 
     def it():
         for t in list(prm.values()) + list(g.values()):
@@ -214,7 +220,10 @@ def cpu_baseline(args, seconds):
         ro_ = ro.clone().requires_grad_(True)
         rd_ = rd.clone().requires_grad_(True)
         d, u, c = O.render_batch_ray(g, prm, dec_b, sc.bound, rd_, ro_, args.stage, dep)
-        loss = ((dep.double() - d).abs() * mask).sum() + 0.2 * (col - c).abs().sum()
+        if kw["loss"] == "mapper":
+            loss = O.mapper_loss(d, c, dep, col, kw["w_color_loss"], kw["color_term"])
+        else:
+            loss = O.tracker_loss(d, u, c, dep, col, kw["w_color_loss"], True, True)
         loss.backward()
 
     it()  # warm-up

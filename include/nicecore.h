@@ -42,12 +42,20 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 2
+#define NC_ABI_VERSION 3
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
 /* nc_*_args.flags */
 #define NC_SAVE_FOR_BACKWARD 1
+
+/* nc_render_args.loss: the rendering loss computed by the core (optional) */
+#define NC_LOSS_NONE 0
+#define NC_LOSS_MAPPER 1  /* src/Mapper.py:603-612: sum_{gt>0} |gt - depth| [+ w * sum |gt_color - color|] */
+#define NC_LOSS_TRACKER 2 /* src/Tracker.py:117-131: sum_mask |gt - depth| / sqrt(unc + 1e-10) [+ w * color] */
+/* nc_render_args.loss_flags */
+#define NC_LOSS_COLOR 1   /* add the colour term (Mapper: stage 'color'; Tracker: use_color_in_tracking) */
+#define NC_LOSS_DYNAMIC 2 /* Tracker handle_dynamic: mask &= tmp < 10 * median(tmp) (<= 16384 rays) */
 
 /* Stage names of render_batch_ray / NICE.forward (decoder.py:341-370). */
 enum nc_stage { NC_STAGE_COARSE = 0, NC_STAGE_MIDDLE = 1, NC_STAGE_FINE = 2, NC_STAGE_COLOR = 3 };
@@ -110,6 +118,18 @@ typedef struct nc_render_args {
   /* backward outputs (NULL = not wanted) */
   float* g_rays_o; /* [N,3] */
   float* g_rays_d; /* [N,3] */
+  /* fused rendering loss (loss != NC_LOSS_NONE): forward writes *loss_out (float64
+   * device scalar, the reference's value incl. its float32 colour sum); backward adds
+   * (*g_loss) * d loss / d (depth, colour) to g_depth / g_color (uncertainty enters the
+   * tracker loss detached, as in the reference). */
+  int32_t loss;             /* NC_LOSS_* */
+  int32_t loss_flags;       /* NC_LOSS_COLOR | NC_LOSS_DYNAMIC */
+  double w_color;           /* w_color_loss (applied in float32, as the reference) */
+  const float* loss_depth;  /* [N] target depth (batch_gt_depth; the coarse mapper renders
+                               without gt_depth but its loss still uses it) */
+  const float* loss_color;  /* [N,3] target colour; required with NC_LOSS_COLOR */
+  double* loss_out;         /* device scalar */
+  const double* g_loss;     /* device scalar upstream gradient of the loss (NULL = 0) */
 } nc_render_args;
 
 typedef struct nc_points_args {

@@ -2,7 +2,7 @@
 //
 // Plans the launches of one render_batch_ray forward / backward:
 //   forward : [k_depth_max] -> k_ray_setup -> k_grid_gather -> k_mlp_fwd (all
-//             decoders of the stage in one launch) -> k_composite_fwd
+//             decoders of the stage in one launch) -> k_composite_fwd -> [k_loss]
 //   backward: k_composite_bwd -> k_mlp_dx (incl. the trilinear backward) ->
 //             [k_mlp_dw -> k_param_reduce] -> [k_ray_grads]
 // Everything is enqueued on the caller's stream; no host synchronisation, no
@@ -36,12 +36,12 @@ int check_hip(int e, const char* what) {
 enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
-  KID_GRID_GATHER, KID_COUNT
+  KID_GRID_GATHER, KID_LOSS, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
-                                       "k_mlp_dw", "k_grid_gather"};
+                                       "k_mlp_dw", "k_grid_gather", "k_loss"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -144,14 +144,15 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0, total = 0;
+  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
+         coef_d = 0, coef_c = 0, total = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
   int slab_wgs = 1;
   int64_t slab_stride = 0;
 };
 
-void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
+void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -168,6 +169,10 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
   w.gocc = take((size_t)P * 4);
   w.grgb = take((size_t)P * 12);
   w.dpts = take((size_t)pl.n_jobs * P * 24);
+  if (loss) {  // per-ray loss derivatives, forward -> backward
+    w.coef_d = take((size_t)N * 8);
+    w.coef_c = take((size_t)N * 12);
+  }
   w.save = save;
   if (save) {
     int64_t r = 0;
@@ -193,7 +198,6 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, Ws& w) {
   w.slab_stride = (max_param_count() + 63) & ~int64_t(63);
   w.slab = take((size_t)pl.n_jobs * w.slab_wgs * w.slab_stride * 4);
   w.total = off;
-  (void)N;
 }
 
 template <typename T>
@@ -253,7 +257,18 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   S = a->n_strat + a->n_surf;
   P = a->n_rays * S;
   if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
-  layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, w);
+  if (a->loss < NC_LOSS_NONE || a->loss > NC_LOSS_TRACKER) return fail(-1, "nicecore: unknown loss " + std::to_string(a->loss));
+  if (a->loss != NC_LOSS_NONE) {
+    if (a->loss_flags & ~(NC_LOSS_COLOR | NC_LOSS_DYNAMIC)) return fail(-1, "nicecore: unknown loss_flags");
+    if ((a->loss_flags & NC_LOSS_DYNAMIC) && a->loss != NC_LOSS_TRACKER)
+      return fail(-1, "nicecore: NC_LOSS_DYNAMIC is the tracker's handle_dynamic");
+    if (!a->loss_out || (a->n_rays > 0 && !a->loss_depth)) return fail(-1, "nicecore: the loss needs loss_depth and loss_out");
+    if ((a->loss_flags & NC_LOSS_COLOR) && a->n_rays > 0 && !a->loss_color)
+      return fail(-1, "nicecore: NC_LOSS_COLOR needs loss_color");
+  } else if (a->loss_flags) {
+    return fail(-1, "nicecore: loss_flags without a loss");
+  }
+  layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w);
   return 0;
 }
 
@@ -294,6 +309,17 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
   c.dpts = at<double>(ws, w.dpts);
   c.g_rays_o = a->g_rays_o;
   c.g_rays_d = a->g_rays_d;
+  c.loss = a->loss;
+  c.loss_flags = a->loss_flags;
+  c.w_color = (float)a->w_color;
+  c.loss_depth = a->loss_depth;
+  c.loss_color = a->loss_color;
+  c.loss_out = a->loss_out;
+  c.g_loss = a->g_loss;
+  if (a->loss != NC_LOSS_NONE) {
+    c.coef_d = at<double>(ws, w.coef_d);
+    c.coef_c = at<float>(ws, w.coef_c);
+  }
 }
 
 int fwd_grid_x(int64_t P, int n_jobs, int which = 0) {
@@ -413,10 +439,13 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   if (int e = render_prepare(a, pl, w, P, S)) return e;
   if (int e = check_models(pl, a->grids, a->dec)) return e;
   if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
-  if (a->n_rays == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a->n_rays == 0) {
+    if (a->loss != NC_LOSS_NONE) return check_hip(hipMemsetAsync(a->loss_out, 0, sizeof(double), s), "loss memset");
+    return 0;
+  }
   if (!a->rays_o || !a->rays_d || !a->depth || !a->var || !a->color)
     return fail(-1, "nicecore: NULL ray input or output pointer");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a->gt_depth && !a->depth_max)
     if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) return e;
   RayCtx rc;
@@ -427,6 +456,8 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(P, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
   if (int e = check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd")) return e;
+  if (a->loss != NC_LOSS_NONE)
+    if (int e = check_hip(timed(KID_LOSS, s, [&] { return launch_loss(rc, s); }), "k_loss")) return e;
   return 0;
 }
 
@@ -461,7 +492,7 @@ static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
   if (int e = plan_stage(a->stage, pl)) return e;
   if (a->n_points < 0) return fail(-1, "nicecore: n_points < 0");
   if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
-  layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, w);
+  layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w);
   return 0;
 }
 

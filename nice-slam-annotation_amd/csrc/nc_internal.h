@@ -85,6 +85,15 @@ struct RayCtx {
   const double* dpts;    // [n_jobs][P][3]
   float* g_rays_o;
   float* g_rays_d;
+  // fused rendering loss (NC_LOSS_*; Mapper.py:603-612, Tracker.py:117-131)
+  int32_t loss, loss_flags;
+  float w_color;             // float32, as the reference's w * color_loss
+  const float* loss_depth;   // [N]
+  const float* loss_color;   // [N][3]
+  double* loss_out;
+  const double* g_loss;
+  double* coef_d;            // [N]    d loss / d depth   (k_loss -> k_composite_bwd)
+  float* coef_c;             // [N][3] d loss / d colour
 };
 
 struct ParamReduceCtx {
@@ -103,6 +112,7 @@ int launch_ray_setup(const RayCtx& c, hipStream_t s);
 int launch_composite_fwd(const RayCtx& c, hipStream_t s);
 int launch_composite_bwd(const RayCtx& c, hipStream_t s);
 int launch_ray_grads(const RayCtx& c, hipStream_t s);
+int launch_loss(const RayCtx& c, hipStream_t s);
 int launch_param_reduce(const ParamReduceCtx& c, int64_t max_nparam, hipStream_t s);
 int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s);
 int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, float* gocc, float* grgb,

@@ -8,6 +8,7 @@
 //                    depth / variance (float64) and colour
 //   k_composite_bwd  its autograd backward: d occupancy and d rgb per sample,
 //                    the transmittance term by a reverse affine wavefront scan
+//   k_loss           the fused Mapper / Tracker rendering loss + per-ray derivatives
 //   k_ray_grads      d rays_o / d rays_d from the per-decoder point gradients
 //   k_param_reduce   sum of the per-workgroup weight-gradient slabs
 // All floating-point expressions keep the reference's association order and the
@@ -228,12 +229,20 @@ __global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
   SampleState s;
   sample_state(c, r, lane, s);
   const double depth = wsum_d((double)s.w * s.z);
-  const double gD = c.g_depth ? c.g_depth[r] : 0.0;
+  double gD = c.g_depth ? c.g_depth[r] : 0.0;
   const double gV = c.g_var ? c.g_var[r] : 0.0;
   float gC[3] = {0.f, 0.f, 0.f};
   if (c.g_color) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) gC[k] = c.g_color[r * 3 + k];
+  }
+  if (c.loss && c.g_loss) {  // the fused loss's contribution (k_loss)
+    const double gl = *c.g_loss;
+    gD = gD + gl * c.coef_d[r];
+    if (c.loss_flags & NC_LOSS_COLOR) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gC[k] = gC[k] + (float)gl * c.coef_c[r * 3 + k];
+    }
   }
   // var = sum w (z-D)^2, D = sum w z  (common.py:253-255)
   const double tmp = s.z - depth;
@@ -269,6 +278,142 @@ __global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) c.grgb[p * 3 + k] = gC[k] * s.w;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_loss -- the rendering loss of the batch and its per-ray derivatives:
+//   NC_LOSS_MAPPER  (Mapper.py:603-612)
+//     loss = sum_{gt>0} |gt - depth|              (float64)
+//            [+ w * sum |gt_c - color|]           (float32 term, NC_LOSS_COLOR)
+//   NC_LOSS_TRACKER (Tracker.py:117-131)
+//     tmp  = |gt - depth| / sqrt(var + 1e-10)     (var detached)
+//     mask = gt > 0 [& tmp < 10 * median(tmp)]    (NC_LOSS_DYNAMIC: handle_dynamic)
+//     loss = sum_mask tmp [+ w * sum_mask |gt_c - color|]
+// One 1024-thread workgroup.  torch.median's lower median (NaN if any tmp is NaN)
+// is a radix select over the float64 bit patterns (tmp >= 0 orders like its bits as
+// unsigned integers): 8 passes of an 8-bit LDS histogram, recomputing tmp from
+// depth/var each pass.  Sums are per-thread strided partials + a fixed-order tree
+// (deterministic).  The colour sum accumulates in float64 and is rounded once to
+// float32 (the reference's float32 sum is pairwise; both are within ~1 ulp of exact).
+// The derivatives are autograd's expressions -- AbsBackward's sgn (sgn(0) = sgn(NaN)
+// = 0), DivBackward's 1/s, SubBackward's negation, masked rows 0 -- and go to
+// coef_d / coef_c, which k_composite_bwd scales by the upstream g_loss.
+// ---------------------------------------------------------------------------
+constexpr int LOSS_THREADS = 1024;
+
+__device__ __forceinline__ double sgn_d(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
+__device__ __forceinline__ float sgn_f(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+__device__ __forceinline__ double tracker_tmp(const RayCtx& c, int64_t r, double& diff, double& s) {
+  diff = (double)c.loss_depth[r] - c.depth[r];
+  s = sqrt(c.var[r] + 1e-10);
+  return fabs(diff) / s;
+}
+
+__global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned long long sel_prefix;
+  __shared__ long long sel_k;
+  __shared__ int any_nan;
+  __shared__ double part_d[LOSS_THREADS / 64], part_c[LOSS_THREADS / 64];
+  const int tid = threadIdx.x;
+  const bool tracker = c.loss == NC_LOSS_TRACKER;
+  const bool dyn = tracker && (c.loss_flags & NC_LOSS_DYNAMIC);
+  const bool col = (c.loss_flags & NC_LOSS_COLOR) != 0;
+  double thr = 0.0;
+  if (dyn) {
+    if (tid == 0) {
+      sel_prefix = 0ull;
+      sel_k = (long long)((c.N - 1) / 2);
+      any_nan = 0;
+    }
+    unsigned long long pmask = 0ull;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0u;
+      __syncthreads();
+      const unsigned long long prefix = sel_prefix;
+      for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
+        double diff, s;
+        const double t = tracker_tmp(c, r, diff, s);
+        if (isnan(t)) {
+          any_nan = 1;
+          continue;
+        }
+        const unsigned long long key = (unsigned long long)__double_as_longlong(t);
+        if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid < 64) {  // wave 0: lane l owns bins 4l..4l+3; find the bin holding rank k
+        unsigned h[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) h[b] = hist[4 * tid + b];
+        const unsigned tot = h[0] + h[1] + h[2] + h[3];
+        unsigned inc = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const unsigned v = __shfl_up(inc, o);
+          if (tid >= o) inc += v;
+        }
+        const long long k = sel_k;
+        const long long exc = (long long)(inc - tot);
+        if (exc <= k && k < (long long)inc) {
+          long long kk = k - exc;
+          int b = 0;
+          while (b < 3 && kk >= (long long)h[b]) kk -= h[b++];
+          sel_k = kk;
+          sel_prefix = prefix | ((unsigned long long)(4 * tid + b) << shift);
+        }
+      }
+      __syncthreads();
+      pmask |= 255ull << shift;
+    }
+    const double med = any_nan ? __longlong_as_double(0x7ff8000000000000ll) : __longlong_as_double((long long)sel_prefix);
+    thr = 10.0 * med;
+  }
+  double sd = 0.0, sc = 0.0;
+  for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
+    const float gt = c.loss_depth[r];
+    bool m = gt > 0.f;
+    double val, coef;
+    if (tracker) {
+      double diff, s;
+      val = tracker_tmp(c, r, diff, s);
+      if (dyn) m = m && (val < thr);
+      coef = -(sgn_d(diff) * (1.0 / s));
+    } else {
+      const double diff = (double)gt - c.depth[r];
+      val = fabs(diff);
+      coef = -sgn_d(diff);
+    }
+    if (m) sd += val;
+    c.coef_d[r] = m ? coef : 0.0;
+    if (col) {
+      const bool mc = tracker ? m : true;  // the mapper's colour term is unmasked
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float dc = c.loss_color[r * 3 + k] - c.color[r * 3 + k];
+        if (mc) sc += (double)fabsf(dc);
+        c.coef_c[r * 3 + k] = mc ? -(c.w_color * sgn_f(dc)) : 0.f;
+      }
+    }
+  }
+  sd = wsum_d(sd);
+  sc = wsum_d(sc);
+  if ((tid & 63) == 0) {
+    part_d[tid >> 6] = sd;
+    part_c[tid >> 6] = sc;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double d = 0.0, cs = 0.0;
+    for (int w = 0; w < LOSS_THREADS / 64; ++w) {
+      d += part_d[w];
+      cs += part_c[w];
+    }
+    double loss = d;
+    if (col) loss = loss + (double)(c.w_color * (float)cs);
+    *c.loss_out = loss;
   }
 }
 
@@ -389,6 +534,10 @@ int launch_composite_fwd(const RayCtx& c, hipStream_t s) {
 }
 int launch_composite_bwd(const RayCtx& c, hipStream_t s) {
   hipLaunchKernelGGL(k_composite_bwd, dim3(ray_blocks(c.N)), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_loss(const RayCtx& c, hipStream_t s) {
+  hipLaunchKernelGGL(k_loss, dim3(1), dim3(LOSS_THREADS), 0, s, c);
   return (int)hipGetLastError();
 }
 int launch_ray_grads(const RayCtx& c, hipStream_t s) {

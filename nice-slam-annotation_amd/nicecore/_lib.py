@@ -12,8 +12,10 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 2
+NC_ABI_VERSION = 3
 NC_SAVE_FOR_BACKWARD = 1
+NC_LOSS_NONE, NC_LOSS_MAPPER, NC_LOSS_TRACKER = 0, 1, 2
+NC_LOSS_COLOR, NC_LOSS_DYNAMIC = 1, 2
 NC_MAX_SAMPLES = 64
 NC_MAX_SURF = 32
 
@@ -48,7 +50,9 @@ class NcRenderArgs(ctypes.Structure):
                 ("grids", NcGrid * 4), ("dec", NcDecoderParams * 4),
                 ("depth", c_void_p), ("var", c_void_p), ("color", c_void_p),
                 ("g_depth", c_void_p), ("g_var", c_void_p), ("g_color", c_void_p),
-                ("g_rays_o", c_void_p), ("g_rays_d", c_void_p)]
+                ("g_rays_o", c_void_p), ("g_rays_d", c_void_p),
+                ("loss", c_int32), ("loss_flags", c_int32), ("w_color", c_double),
+                ("loss_depth", c_void_p), ("loss_color", c_void_p), ("loss_out", c_void_p), ("g_loss", c_void_p)]
 
 
 class NcPointsArgs(ctypes.Structure):
@@ -110,7 +114,7 @@ def check(rc: int, what: str):
 KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_fwd": 3,
               "k_composite_bwd": 4, "k_mlp_dx": 5, "k_param_reduce": 6, "k_ray_grads": 7,
               "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10,
-              "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13}
+              "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14}
 
 
 class KernelTimer:

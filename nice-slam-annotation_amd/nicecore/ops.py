@@ -36,3 +36,45 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max}
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
+
+
+_LOSS_KINDS = {"mapper": L.NC_LOSS_MAPPER, "tracker": L.NC_LOSS_TRACKER}
+
+
+def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, loss="mapper",
+                     target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
+                     gt_depth="target", n_strat=32, n_surf=16, depth_max=None):
+    """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
+    color, loss) with ``loss`` a float64 device scalar that backpropagates into the
+    grids / decoders / rays like the reference's loss expression:
+
+    ``loss="mapper"``  (src/Mapper.py:603-612)
+        sum_{target_depth>0} |target_depth - depth|  [+ w_color * sum |target_color - color|]
+    ``loss="tracker"`` (src/Tracker.py:117-131; uncertainty detached)
+        tmp = |target_depth - depth| / sqrt(uncertainty + 1e-10)
+        mask = target_depth > 0 [& tmp < 10 * tmp.median()]  (handle_dynamic)
+        sum_mask tmp  [+ w_color * sum_mask |target_color - color|]
+
+    ``color_term`` adds the colour term (Mapper: stage == 'color' or not nice; Tracker:
+    use_color_in_tracking).  ``gt_depth`` is the depth that guides the surface samples;
+    by default the target itself (the tracker and the non-coarse mapper); the coarse
+    mapper renders with None."""
+    if loss not in _LOSS_KINDS:
+        raise L.NiceCoreError(f"loss must be one of {sorted(_LOSS_KINDS)}")
+    if handle_dynamic and loss != "tracker":
+        raise L.NiceCoreError("handle_dynamic is the tracker's outlier mask")
+    if color_term and target_color is None:
+        raise L.NiceCoreError("color_term needs target_color")
+    flags = (L.NC_LOSS_COLOR if color_term else 0) | (L.NC_LOSS_DYNAMIC if handle_dynamic else 0)
+    if isinstance(gt_depth, str):
+        gt_depth = target_depth
+    if stage == 'coarse':
+        gt_depth = None
+    ns = n_surf if gt_depth is not None else 0
+    if n_strat + ns > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
+        raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
+    plan = make_plan(stage, decoders)
+    spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
+            "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth,
+                     target_color if color_term else None)}
+    return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())

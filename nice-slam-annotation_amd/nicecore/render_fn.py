@@ -1,7 +1,8 @@
 """torch.autograd.Function wrappers around libnicecore.so.
 
 ``NiceRenderFn``   = Renderer.render_batch_ray (src/utils/Renderer.py:95-262) forward +
-                     autograd backward, in two C-ABI calls.
+                     autograd backward, in two C-ABI calls; optionally with the
+                     Mapper / Tracker rendering loss fused in (a 4th output).
 ``NiceEvalFn``     = NICE.forward (src/conv_onet/models/decoder.py:336-370) on caller
                      points.
 
@@ -298,7 +299,10 @@ def _split_param_grads(plan, flats, needs_params):
 
 class NiceRenderFn(torch.autograd.Function):
     """render_batch_ray on the HIP core.  Inputs: (spec, rays_o, rays_d, gt_depth|None,
-    grid_coarse|None, grid_middle|None, grid_fine|None, grid_color|None, *params)."""
+    grid_coarse|None, grid_middle|None, grid_fine|None, grid_color|None, *params).
+    Outputs (depth, var, color), plus the float64 scalar loss when ``spec["loss"]`` =
+    (kind, flags, w_color, target_depth, target_color|None) asks for one (targets
+    are data: no gradient flows to them, as in the reference)."""
 
     @staticmethod
     def forward(ctx, spec, rays_o, rays_d, gt_depth, g0, g1, g2, g3, *params):
@@ -337,6 +341,17 @@ class NiceRenderFn(torch.autograd.Function):
         var = torch.empty(N, device=device, dtype=torch.float64)
         color = torch.empty(N, 3, device=device, dtype=torch.float32)
         a.depth, a.var, a.color = depth.data_ptr(), var.data_ptr(), color.data_ptr()
+        loss_spec = spec.get("loss")
+        loss = tgt = None
+        if loss_spec is not None:
+            kind, lflags, w, tdepth, tcolor = loss_spec
+            tgt = (tdepth.detach().reshape(-1).float().contiguous(),
+                   tcolor.detach().reshape(-1, 3).float().contiguous() if tcolor is not None else None)
+            if tgt[0].shape[0] != N or (tgt[1] is not None and tgt[1].shape[0] != N):
+                raise L.NiceCoreError("loss targets must have one row per ray")
+            loss = torch.empty((), device=device, dtype=torch.float64)
+            a.loss, a.loss_flags, a.w_color = kind, lflags, float(w)
+            a.loss_depth, a.loss_color, a.loss_out = tgt[0].data_ptr(), _ptr(tgt[1]), loss.data_ptr()
         nbytes = lib.nc_render_workspace_bytes(ctypes.byref(a))
         if nbytes == 0:
             L.check(-1, "nc_render_workspace_bytes")
@@ -344,12 +359,14 @@ class NiceRenderFn(torch.autograd.Function):
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_render_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_render_forward")
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
-        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params)
+        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt)
         ctx.grids = grids
-        return depth, var, color
+        if loss is None:
+            return depth, var, color
+        return depth, var, color, loss
 
     @staticmethod
-    def backward(ctx, g_depth, g_var, g_color):
+    def backward(ctx, g_depth, g_var, g_color, g_loss=None):
         lib = L.load()
         a, plan = ctx.args, ctx.plan
         need = ctx.needs_input_grad
@@ -359,6 +376,8 @@ class NiceRenderFn(torch.autograd.Function):
         gv = g_var.detach().double().contiguous() if g_var is not None else None
         gc = g_color.detach().float().contiguous() if g_color is not None else None
         a.g_depth, a.g_var, a.g_color = _ptr(gd), _ptr(gv), _ptr(gc)
+        gl = g_loss.detach().double().reshape(1).contiguous() if g_loss is not None else None
+        a.g_loss = _ptr(gl)
         g_ro = torch.empty_like(rays_o) if need[1] else None
         g_rd = torch.empty_like(rays_o) if need[2] else None
         # the kernel computes d rays_o and d rays_d together; ask for both if either is needed

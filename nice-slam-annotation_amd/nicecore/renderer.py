@@ -10,6 +10,9 @@ src/Tracker.py / src/Mapper.py / src/utils/Visualizer.py call it unchanged:
   render_img(c, decoders, c2w, device, stage, gt_depth=None)
       -> (depth [H,W], uncertainty [H,W], color [H,W,3])              Renderer.py:264
 
+plus ``render_batch_loss`` (extension): render_batch_ray with the Mapper's / Tracker's
+loss expression (Mapper.py:603-612, Tracker.py:117-131) computed in the same launches.
+
 Only the configuration the NICE configs use is implemented (N_importance = 0,
 lindisp = False, perturb = 0, occupancy = True; configs/nice_slam.yaml:5,121-126);
 anything else raises instead of silently falling back.
@@ -20,7 +23,7 @@ import torch
 
 from . import _lib as L
 from .ops import eval_points as _eval_points
-from .ops import render_rays
+from .ops import render_rays, render_rays_loss
 
 
 class Renderer(object):
@@ -70,6 +73,19 @@ class Renderer(object):
             gt_depth = gt_depth.reshape(-1)
         return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
                            self.N_samples, self.N_surface, depth_max)
+
+    def render_batch_loss(self, c, decoders, rays_d, rays_o, device, stage, gt_depth, gt_color=None,
+                          loss='mapper', w_color_loss=0.2, color_term=False, handle_dynamic=False,
+                          render_gt_depth='target', depth_max=None):
+        """render_batch_ray + the rendering loss (ops.render_rays_loss): returns
+        (depth, uncertainty, color, loss).  Mapper.optimize_map:
+        ``loss='mapper', color_term=(not nice) or stage == 'color',
+        render_gt_depth=None if coarse_mapper else 'target'``; Tracker.optimize_cam_in_batch:
+        ``loss='tracker', color_term=use_color_in_tracking, handle_dynamic=handle_dynamic``."""
+        self._check_supported()
+        return render_rays_loss(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth.reshape(-1),
+                                loss, gt_color, w_color_loss, color_term, handle_dynamic,
+                                render_gt_depth, self.N_samples, self.N_surface, depth_max)
 
     def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
         """Renderer.py:264-340: chunked full-image render, no grad."""

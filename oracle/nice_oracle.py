@@ -189,6 +189,37 @@ def render_batch_ray(grids, prm, dec_bounds, bound, rays_d, rays_o, stage, gt_de
     return depth, var, color
 
 
+def mapper_loss(depth, color, gt_depth, gt_color=None, w_color=0.2, color_term=False):
+    """Mapper.optimize_map's rendering loss (Mapper.py:603-612, nice=True, occupancy on):
+    L1 depth over gt > 0 (float64) plus, in the 'color' stage, w_color times the
+    unmasked float32 L1 colour sum.  Parity of the loss itself is UNPINNED (the
+    reference's loss lives inside Mapper.optimize_map; no fixture holds it) -- its
+    inputs, the render outputs, are pinned by tests/golden."""
+    m = gt_depth > 0
+    loss = torch.abs(gt_depth[m] - depth[m]).sum()
+    if color_term:
+        loss = loss + w_color * torch.abs(gt_color - color).sum()
+    return loss
+
+
+def tracker_loss(depth, var, color, gt_depth, gt_color=None, w_color=0.5, color_term=True,
+                 handle_dynamic=True):
+    """Tracker.optimize_cam_in_batch's loss (Tracker.py:117-131): depth residual scaled
+    by the detached render uncertainty, rays with gt > 0 (and, with handle_dynamic,
+    residual < 10 x its lower median -- torch.median) only; the optional colour term
+    uses the same mask.  Parity unpinned, as mapper_loss."""
+    var = var.detach()
+    scaled = torch.abs(gt_depth - depth) / torch.sqrt(var + 1e-10)
+    if handle_dynamic:
+        mask = (scaled < 10 * scaled.median()) & (gt_depth > 0)
+    else:
+        mask = gt_depth > 0
+    loss = scaled[mask].sum()
+    if color_term:
+        loss = loss + w_color * torch.abs(gt_color - color)[mask].sum()
+    return loss
+
+
 def points_for_rays(rays_o, rays_d, bound, gt_depth, stage, n_strat=32, n_surf=16):
     """The float64 sample points render_batch_ray evaluates (Renderer.py:227-231)."""
     if stage == 'coarse':

@@ -64,3 +64,27 @@ def test_bad_args_fail_loudly(lib):
     a.stage = 7
     assert lib.nc_render_forward(ctypes.byref(a), None, 0, None) < 0
     assert b"stage" in lib.nc_last_error()
+
+
+def test_loss_args_validated(lib):
+    """The fused-loss fields (ABI v3) are checked before any launch."""
+    def args(**kw):
+        a = L.NcRenderArgs()
+        a.abi_version = L.NC_ABI_VERSION
+        a.stage = L.STAGES["color"]
+        a.n_rays, a.n_strat, a.n_surf = 4, 32, 0
+        for k, v in kw.items():
+            setattr(a, k, v)
+        return a
+
+    for kw, msg in ((dict(loss=5), b"unknown loss"),
+                    (dict(loss_flags=L.NC_LOSS_COLOR), b"without a loss"),
+                    (dict(loss=L.NC_LOSS_MAPPER), b"loss_depth and loss_out"),
+                    (dict(loss=L.NC_LOSS_MAPPER, loss_flags=L.NC_LOSS_DYNAMIC, loss_out=8, loss_depth=8),
+                     b"handle_dynamic"),
+                    (dict(loss=L.NC_LOSS_TRACKER, loss_flags=L.NC_LOSS_COLOR, loss_out=8, loss_depth=8),
+                     b"loss_color"),
+                    (dict(loss=L.NC_LOSS_TRACKER, loss_flags=8, loss_out=8, loss_depth=8), b"loss_flags")):
+        a = args(**kw)
+        assert lib.nc_render_workspace_bytes(ctypes.byref(a)) == 0, kw
+        assert msg in lib.nc_last_error(), (kw, lib.nc_last_error())
