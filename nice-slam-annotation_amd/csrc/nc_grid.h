@@ -52,10 +52,13 @@ __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners&
 
 // Grid-gradient scatter of one wave's 16 points (grid_sampler_3d_backward's
 // gInput += w_k * gOut).  The point features' gradients (C layout) and corner
-// tables go through a private LDS slice, then every float atomic instruction
-// covers whole 128-byte corner rows (lane = channel, the two half-waves take
-// different points), and consecutive samples of a ray that fall in the same
-// voxel cell are summed on chip first (one atomic per corner per run).
+// tables go through a private LDS slice.  Lane = (x side of the corner, channel):
+// both half-waves walk the same 16 samples in lockstep, each holding the 4 corners
+// of its x side, so every control decision is wave-uniform and every float atomic
+// instruction covers two whole, adjacent 128-B corner rows (x0 and x0+1 of one
+// (y, z): contiguous in channels-last).  Consecutive samples of a ray in the same
+// voxel cell are summed on chip (one add per corner per run); a step to a
+// face-adjacent cell carries the shared face over.
 constexpr int SCAT_FLOATS = 16 * 32 + 16 * 8 + 2 * 16 * 8 + 2 * 16 + 16 + 16;  // 976 (16-B multiple)
 
 __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c, const float dc[8], bool valid,
@@ -67,9 +70,7 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
   int* INB = reinterpret_cast<int*>(reg + 928);             // [16] in-bounds corner mask
   *reinterpret_cast<float4*>(D + i * 32 + 4 * g) = float4{dc[0], dc[1], dc[2], dc[3]};
   *reinterpret_cast<float4*>(D + i * 32 + 16 + 4 * g) = float4{dc[4], dc[5], dc[6], dc[7]};
-  // lane-group g writes corners 2g, 2g+1 of its point
   {
-    // corners 2g, 2g+1: x bit = h, y bit = g&1, z bit = g>>1 (selects, not a runtime index)
     const int yb = g & 1, zb = g >> 1;
     const float wy = yb ? c.wy[1] : c.wy[0];
     const float wz = zb ? c.wz[1] : c.wz[0];
@@ -80,7 +81,6 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
     OFF[i * 8 + 2 * g + 1] = base + G.grad_stride[3];
   }
   if (g == 0) {
-    // cell coordinates packed into the key (x | y << 21 | z << 42; grids < 2^21 per axis)
     KEY[i] = valid ? (c.x0 | (c.y0 << 21) | (c.z0 << 42)) : -1;
     INB[i] = valid ? (int)c.inb : 0;
   }
@@ -89,23 +89,17 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int half = lane >> 5, ch = lane & 31;
   const int64_t chs = (int64_t)ch * G.grad_stride[0];
-  float acc[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  // Walk the half's 8 samples in order.  acc[k] holds corner k of the current cell.
-  // Same cell: keep accumulating.  Next cell one step away along one axis: the 4
-  // corners of the shared face carry over, the other 4 are flushed.  Otherwise all
-  // 8 are flushed.  One atomic instruction = one 128-B corner row (lane = channel).
-  int run = half * 8;
-  int64_t cur = KEY[run];
-  auto flush_k = [&](int pt, int k) {
-    if ((INB[pt] >> k) & 1) atomicAdd(G.grad + OFF[pt * 8 + k] + chs, acc[k]);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto flush = [&](int pt, int xb, int q, float v) {
+    const int k = xb | (q << 1);
+    if ((INB[pt] >> k) & 1) atomicAdd(G.grad + OFF[pt * 8 + k] + chs, v);
   };
-  for (int j = 0; j < 8; ++j) {
-    const int pt = half * 8 + j;
-    const int64_t kk = KEY[pt];
+  int run = 0;
+  int64_t cur = KEY[0];
+  for (int pt = 0; pt < 16; ++pt) {
+    const int64_t kk = KEY[pt];  // wave-uniform
     if (kk != cur) {
-      const int64_t d = kk - cur;  // exact for one-step moves (no borrow across fields)
+      const int64_t d = kk - cur;
       int axis = -1, dir = 0;
       if (cur >= 0 && kk >= 0) {
         if (d == 1) { axis = 0; dir = 1; }
@@ -117,35 +111,42 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
       }
       if (axis < 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { flush_k(run, k); acc[k] = 0.f; }
+        for (int q = 0; q < 4; ++q) {
+          flush(run, half, q, acc[q]);
+          acc[q] = 0.f;
+        }
+      } else if (axis == 0) {
+        const int L = dir > 0 ? 0 : 1;
+        float mv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mv[q] = __shfl_xor(acc[q], 32);
+        const bool onL = half == L;
+        flush(run, L, onL ? 0 : 2, onL ? acc[0] : mv[2]);
+        flush(run, L, onL ? 1 : 3, onL ? acc[1] : mv[3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = onL ? mv[q] : 0.f;
       } else {
-        // corners with the axis bit == (dir > 0 ? 1 : 0) form the shared face: they
-        // become the new cell's corners with the bit flipped
-        const int bit = 1 << axis;
+        const int qb = axis;
+        float nacc[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const bool leaving = ((k & bit) != 0) == (dir < 0);  // face not shared
-          if (leaving) flush_k(run, k);
-        }
-        float nacc[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int src = k ^ bit;  // same corner in the old cell's numbering
-          const bool from_old = ((k & bit) != 0) == (dir < 0);
-          nacc[k] = from_old ? acc[src] : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          const bool other = ((q & qb) != 0) == (dir < 0);
+          if (other) flush(run, half, q, acc[q]);
+          nacc[q] = other ? acc[q ^ qb] : 0.f;
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = nacc[k];
+        for (int q = 0; q < 4; ++q) acc[q] = nacc[q];
       }
       cur = kk;
     }
     const float dv = D[pt * 32 + ch];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = acc[k] + Wt[pt * 8 + k] * dv;
+    for (int q = 0; q < 4; ++q) acc[q] = acc[q] + Wt[pt * 8 + half + 2 * q] * dv;
     run = pt;
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) flush_k(run, k);
+  for (int q = 0; q < 4; ++q) flush(run, half, q, acc[q]);
 }
+
 
 }  // namespace nc

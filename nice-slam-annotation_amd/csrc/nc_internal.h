@@ -134,7 +134,13 @@ int64_t max_param_count();
 
 constexpr int FWD_TILES = 1;      // 16-point tiles per wave (2: interleaved chains, 248 VGPRs: slower)
 constexpr int FWD_THREADS = 768;  // 12 waves, 192 points per WG iteration; measured best of 512/768/1024
-constexpr int DX_THREADS = 768;   // 12 waves x 16 points, barrier-free; 3 waves/SIMD at <= 170 VGPRs
-constexpr int DW_THREADS = 1024;  // 16 waves own the dW tiles; 32-point sub-chunks
+#ifndef NC_DX_THREADS
+#define NC_DX_THREADS 768
+#endif
+constexpr int DX_THREADS = NC_DX_THREADS;   // 12 waves x 16 points, barrier-free; 3 waves/SIMD at <= 170 VGPRs
+#ifndef NC_DW_THREADS
+#define NC_DW_THREADS 1024
+#endif
+constexpr int DW_THREADS = NC_DW_THREADS;  // 16 waves own the dW tiles; 32-point sub-chunks
 
 }  // namespace nc

@@ -467,7 +467,7 @@ __host__ __device__ constexpr int cmax_(int a, int b) { return a > b ? a : b; }
 // k_mlp_dx LDS: its weight image, then one grid-scatter slice per wave
 constexpr int DX_SLICE_BASE = cmax_(cmax_(Net<K_COARSE, PADW_BWD>::WEIGHTS, Net<K_MID, PADW_BWD>::WEIGHTS),
                                     cmax_(Net<K_FINE, PADW_BWD>::WEIGHTS, Net<K_COLOR, PADW_BWD>::WEIGHTS));
-static_assert(DX_SLICE_BASE % 4 == 0, "scatter slices hold int64 arrays");
+static_assert(DX_SLICE_BASE % 4 == 0, "scatter slices are float4-aligned");
 constexpr int DX_LDS_FLOATS = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
 static_assert(DX_LDS_FLOATS * 4 <= 160 * 1024, "dX LDS budget");
 
@@ -591,7 +591,11 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         dcv[r] = valid ? dc[0][r] : 0.f;
         dcv[4 + r] = valid ? dc[1][r] : 0.f;
       }
+#ifndef NC_ABL_DX_NO_COORD  // timing-only ablation: no coordinate gradient
       if (need_coord) {
+#else
+      if (false) {
+#endif
         float gi[3];
         if (grid_vec_ok(G)) grid_coord_grad<true>(G, co, dcv, g, gi);
         else grid_coord_grad<false>(G, co, dcv, g, gi);
@@ -604,7 +608,9 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
           gg[k] = ((double)gk * 2.0) / (D.bound[k][1] - D.bound[k][0]);
         }
       }
+#ifndef NC_ABL_DX_NO_SCATTER  // timing-only ablation: no grid scatter
       if (need_grid) grid_scatter(G, co, dcv, valid, slice, i, g, lane);
+#endif
     }
     if (need_coord && valid && g == 0) {
       double* dst = ctx.dpts + ((int64_t)job.slot * ctx.P + p) * 3;
@@ -636,7 +642,10 @@ __global__ void __launch_bounds__(DX_THREADS) k_mlp_dx(const MlpCtx ctx) {
 // registers; bias gradients (row sums of dY) go to LDS float atomics.  One flush
 // per workgroup into a slab, summed by k_param_reduce.
 // ---------------------------------------------------------------------------
-constexpr int DW_NPTS = 32;  // points per staged sub-chunk (8 MFMA k-steps)
+#ifndef NC_DW_NPTS
+#define NC_DW_NPTS 32
+#endif
+constexpr int DW_NPTS = NC_DW_NPTS;  // points per staged sub-chunk (8 MFMA k-steps)
 
 template <int KIND>
 struct DwLayout {
@@ -793,10 +802,13 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
   for (int64_t sub = blockIdx.x; sub < nsub; sub += gridDim.x) {
     __syncthreads();  // previous sub-chunk's reads are done
     const int64_t p0 = sub * DW_NPTS;
+#ifndef NC_ABL_DW_NO_STAGE  // timing-only ablation: records not copied into LDS
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (dst[k] >= 0) *reinterpret_cast<float4*>(buf + dst[k]) = pre[k];
+#endif
     __syncthreads();
+#ifndef NC_ABL_DW_NO_EMB  // timing-only ablation: no Fourier recompute
     if constexpr (N::XYZ) {  // Fourier features, exactly as wave_forward computes them
       // (rows past P hold p = 0 and padded B columns are 0: sin(0) = 0, no checks)
       const float* B = lds + LY::FB;
@@ -807,6 +819,8 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
             NC_SIN(__builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m])));
       }
     }
+#endif
+#ifndef NC_ABL_DW_NO_MASKPASS  // timing-only ablation: no dZ pass
     // dZ_L = dh_L * relu'(Z_L) (mask bit 8L+j of lane-group g's word; L = 4: hi word)
     for (int e = threadIdx.x; e < DW_NPTS * 40; e += DW_THREADS) {
       const int r = e / 40, c4 = e - r * 40, L = c4 >> 3, jj = c4 & 7;
@@ -817,13 +831,19 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
       *reinterpret_cast<float4*>(row + LY::DZ + HID * L + 4 * jj) =
           float4{(w & 1u) ? dh.x : 0.f, (w & 2u) ? dh.y : 0.f, (w & 4u) ? dh.z : 0.f, (w & 8u) ? dh.w : 0.f};
     }
+#endif
     __syncthreads();
+#ifndef NC_ABL_DW_NO_LOAD  // timing-only ablation: the next records are not loaded
     if (sub + gridDim.x < nsub) prefetch(sub + gridDim.x);
+#endif
     // ---- tiles: DW_NPTS/4 k-steps of 4 points; the wave's NS accumulation chains are
     // interleaved (k-step outer) so no MFMA waits on its predecessor's result ----
     // one k-step = NS independent MFMAs + 2 NS reads at immediate offsets; unrolled by
     // 4 with a scheduling barrier per k-step (fully unrolled, the scheduler hoists
     // every k-step's reads and spills)
+#ifdef NC_ABL_DW_NO_MFMA  // timing-only ablation: no k-steps
+    if (false)
+#endif
 #pragma unroll 4
     for (int q = 0; q < DW_NPTS / 4; ++q) {
       __builtin_amdgcn_sched_barrier(0);

@@ -19,6 +19,15 @@ VARIANTS = {
     "no_mask": ["-DNC_ABL_NO_MASK"],
     "fwd_nolds": ["-DNC_ABL_FWD_NOLDS"],
     "fwd_nolds_notrig": ["-DNC_ABL_FWD_NOLDS", "-DNC_ABL_NO_TRIG", "-DNC_ABL_NO_RECSTORE"],
+    "dx_no_scatter": ["-DNC_ABL_DX_NO_SCATTER"],
+    "dx_no_atomic": ["-DNC_ABL_DX_NO_ATOMIC"],
+    "dx_no_coord": ["-DNC_ABL_DX_NO_COORD"],
+    "dx_no_trilinear": ["-DNC_ABL_DX_NO_SCATTER", "-DNC_ABL_DX_NO_COORD"],
+    "dx512": ["-DNC_DX_THREADS=512"],
+    "dw512_16": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=16"],
+    "dw256_16": ["-DNC_DW_THREADS=256", "-DNC_DW_NPTS=16"],
+    "dw1024_16": ["-DNC_DW_THREADS=1024", "-DNC_DW_NPTS=16"],
+    "dw512_32": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=32"],
     "dw_no_emb": ["-DNC_ABL_DW_NO_EMB"],
     "dw_no_maskpass": ["-DNC_ABL_DW_NO_MASKPASS"],
     "dw_no_stage": ["-DNC_ABL_DW_NO_STAGE"],
