@@ -48,6 +48,10 @@ extern "C" {
 
 /* nc_*_args.flags */
 #define NC_SAVE_FOR_BACKWARD 1
+/* Grid gradients by an ordered reduction instead of float atomics: bit-identical run
+ * to run, summed per voxel in the reference's order (ascending point, corner).  Set it
+ * on the forward (it sizes the workspace) and keep it for the backward. */
+#define NC_DETERMINISTIC 2
 
 /* nc_render_args.loss: the rendering loss computed by the core (optional) */
 #define NC_LOSS_NONE 0

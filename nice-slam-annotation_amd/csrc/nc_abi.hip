@@ -36,12 +36,12 @@ int check_hip(int e, const char* what) {
 enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
-  KID_GRID_GATHER, KID_LOSS, KID_COUNT
+  KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
-                                       "k_mlp_dw", "k_grid_gather", "k_loss"};
+                                       "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -145,14 +145,17 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 
 struct Ws {
   size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
-         coef_d = 0, coef_c = 0, total = 0;
+         coef_d = 0, coef_c = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dtemp = 0, dtemp_bytes = 0,
+         total = 0;
+  bool det = false;
+  int vbits = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
   int slab_wgs = 1;
   int64_t slab_stride = 0;
 };
 
-void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w) {
+void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -197,6 +200,19 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
   w.slab_wgs = (int)((blocks < per_job) ? (blocks > 0 ? blocks : 1) : per_job);
   w.slab_stride = (max_param_count() + 63) & ~int64_t(63);
   w.slab = take((size_t)pl.n_jobs * w.slab_wgs * w.slab_stride * 4);
+  if (save && vbits > 0) {  // NC_DETERMINISTIC grid-gradient buffers (nc_det.hip)
+    const int64_t ne = (int64_t)pl.n_jobs * P * 8;
+    w.det = true;
+    w.vbits = vbits;
+    w.dfeat = take((size_t)pl.n_jobs * P * 32 * 4);
+    for (int b = 0; b < 2; ++b) {
+      w.dkey[b] = take((size_t)ne * 8);
+      w.dval[b] = take((size_t)ne * 4);
+    }
+    w.dw = take((size_t)ne * 4);
+    w.dtemp_bytes = det_sort_temp_bytes(ne, vbits + 2);
+    w.dtemp = take(w.dtemp_bytes);
+  }
   w.total = off;
 }
 
@@ -243,6 +259,33 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.slab = at<float>(ws, w.slab);
   m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
   m.cfeat = w.save ? m.rec : at<float>(ws, w.feat);
+  m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
+}
+
+DetBufs det_bufs(void* ws, const Ws& w) {
+  DetBufs d;
+  for (int b = 0; b < 2; ++b) {
+    d.key[b] = at<uint64_t>(ws, w.dkey[b]);
+    d.val[b] = at<uint32_t>(ws, w.dval[b]);
+  }
+  d.w = at<float>(ws, w.dw);
+  d.temp = at<void>(ws, w.dtemp);
+  d.temp_bytes = w.dtemp_bytes;
+  d.vbits = w.vbits;
+  return d;
+}
+
+// NC_DETERMINISTIC: voxel-index bits over the grids the stage's decoders sample
+int stage_vbits(const Plan& pl, const nc_grid* grids) {
+  uint64_t most = 1;
+  for (int j = 0; j < pl.n_jobs; ++j) {
+    const nc_grid& G = grids[pl.jobs[j].kind];
+    const uint64_t v = (uint64_t)G.dims[0] * (uint64_t)G.dims[1] * (uint64_t)G.dims[2];
+    if (v > most) most = v;
+  }
+  int b = 1;
+  while ((uint64_t(1) << b) < most) ++b;
+  return b;
 }
 
 int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S) {
@@ -256,7 +299,7 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
   S = a->n_strat + a->n_surf;
   P = a->n_rays * S;
-  if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
+  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC)) return fail(-1, "nicecore: unknown flags");
   if (a->loss < NC_LOSS_NONE || a->loss > NC_LOSS_TRACKER) return fail(-1, "nicecore: unknown loss " + std::to_string(a->loss));
   if (a->loss != NC_LOSS_NONE) {
     if (a->loss_flags & ~(NC_LOSS_COLOR | NC_LOSS_DYNAMIC)) return fail(-1, "nicecore: unknown loss_flags");
@@ -268,7 +311,14 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   } else if (a->loss_flags) {
     return fail(-1, "nicecore: loss_flags without a loss");
   }
-  layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w);
+  int vbits = -1;
+  if (a->flags & NC_DETERMINISTIC) {
+    vbits = stage_vbits(pl, a->grids);
+    if (vbits > 60 || (int64_t)pl.n_jobs * P * 8 >= (int64_t(1) << 32))
+      return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
+  }
+  layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w, vbits);
+  if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }
 
@@ -345,9 +395,13 @@ int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s);
 
 // decoder backward: dX chains + trilinear backward (k_mlp_dx) -> weight gradients
 // -> slab reduction
-int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s) {
+int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s, const DetBufs* det) {
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
   if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs, 1), s); }), "k_mlp_dx")) return e;
+  bool any_grid = false;
+  for (int j = 0; j < m.n_jobs; ++j) any_grid |= m.jobs[j].need_grid != 0;
+  if (m.dfeat && any_grid)
+    if (int e = check_hip(timed(KID_DET_SCATTER, s, [&] { return launch_det_scatter(m, *det, s); }), "deterministic grid scatter")) return e;
   bool any_dw = false;
   for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;
   if (any_dw)
@@ -480,7 +534,8 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   for (int j = 0; j < m.n_jobs; ++j) any |= m.jobs[j].need_dw || m.jobs[j].need_grid;
   if (!any) return 0;
   if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
-  if (int e = mlp_backward(m, a->dec, P, s)) return e;
+  const DetBufs det = det_bufs(ws, w);
+  if (int e = mlp_backward(m, a->dec, P, s, &det)) return e;
   if (need_coord)
     if (int e = check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(rc, s); }), "k_ray_grads")) return e;
   return 0;
@@ -491,8 +546,15 @@ static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
   if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
   if (int e = plan_stage(a->stage, pl)) return e;
   if (a->n_points < 0) return fail(-1, "nicecore: n_points < 0");
-  if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
-  layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w);
+  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC)) return fail(-1, "nicecore: unknown flags");
+  int vbits = -1;
+  if (a->flags & NC_DETERMINISTIC) {
+    vbits = stage_vbits(pl, a->grids);
+    if (vbits > 60 || (int64_t)pl.n_jobs * a->n_points * 8 >= (int64_t(1) << 32))
+      return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
+  }
+  layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w, vbits);
+  if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }
 
@@ -533,7 +595,8 @@ int nc_points_backward(const nc_points_args* a, void* ws, size_t ws_bytes, void*
   fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, a->g_pts != nullptr);
   if (int e = check_hip(timed(KID_POINTS_SPLIT, s, [&] { return launch_points_split_grad(m, a->stage, a->g_raw, (float*)m.gocc, (float*)m.grgb, s); }), "k_points_split_grad"))
     return e;
-  if (int e = mlp_backward(m, a->dec, a->n_points, s)) return e;
+  const DetBufs det = det_bufs(ws, w);
+  if (int e = mlp_backward(m, a->dec, a->n_points, s, &det)) return e;
   if (a->g_pts)
     if (int e = check_hip(timed(KID_POINTS_GRADS, s, [&] { return launch_points_grads(m, a->g_pts, s); }), "k_points_grads")) return e;
   return 0;

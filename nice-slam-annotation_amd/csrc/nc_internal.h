@@ -48,7 +48,25 @@ struct MlpCtx {
                              // by backward activations (k_mlp_dx); both read by k_mlp_dw
   float* slab;               // [n_jobs][slab_wgs][slab_stride] per-workgroup parameter gradients
   int64_t slab_stride;
+  float* dfeat;              // NC_DETERMINISTIC: [n_jobs][P][32] d features of each job's own grid
+                             // (k_mlp_dx stores them instead of scattering with atomics), else NULL
 };
+
+// NC_DETERMINISTIC grid-gradient scatter (nc_det.hip): every (job, point, corner)
+// contribution becomes an entry keyed by (job, voxel); a stable radix sort groups the
+// entries of one voxel in ascending (point, corner) order -- the reference's own
+// accumulation order (ATen's CPU grid_sampler_3d_backward) -- and one owner per voxel
+// sums them in that order.  Run to run bit-identical.
+struct DetBufs {
+  uint64_t* key[2];          // [n_jobs * P * 8] sort keys in / out
+  uint32_t* val[2];          // entry ids in / out
+  float* w;                  // [n_jobs * P * 8] trilinear weight of each entry
+  void* temp;                // rocprim radix-sort scratch
+  size_t temp_bytes;
+  int32_t vbits;             // bits of the voxel index; key = job << vbits | voxel
+};
+size_t det_sort_temp_bytes(int64_t n_entries, int end_bit);
+int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s);
 
 // Arguments of the per-ray kernels (sampling, compositing, ray gradients).
 struct RayCtx {

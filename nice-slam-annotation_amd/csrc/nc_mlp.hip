@@ -609,7 +609,17 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         }
       }
 #ifndef NC_ABL_DX_NO_SCATTER  // timing-only ablation: no grid scatter
-      if (need_grid) grid_scatter(G, co, dcv, valid, slice, i, g, lane);
+      if (need_grid) {
+        if (ctx.dfeat) {  // NC_DETERMINISTIC: ordered reduction in nc_det.hip instead of atomics
+          if (valid) {
+            float* df = ctx.dfeat + ((int64_t)job.slot * ctx.P + p) * 32;
+            *reinterpret_cast<float4*>(df + 4 * g) = float4{dcv[0], dcv[1], dcv[2], dcv[3]};
+            *reinterpret_cast<float4*>(df + 16 + 4 * g) = float4{dcv[4], dcv[5], dcv[6], dcv[7]};
+          }
+        } else {
+          grid_scatter(G, co, dcv, valid, slice, i, g, lane);
+        }
+      }
 #endif
     }
     if (need_coord && valid && g == 0) {

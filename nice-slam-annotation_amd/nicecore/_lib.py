@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
 NC_ABI_VERSION = 3
 NC_SAVE_FOR_BACKWARD = 1
+NC_DETERMINISTIC = 2
 NC_LOSS_NONE, NC_LOSS_MAPPER, NC_LOSS_TRACKER = 0, 1, 2
 NC_LOSS_COLOR, NC_LOSS_DYNAMIC = 1, 2
 NC_MAX_SAMPLES = 64
@@ -114,7 +115,7 @@ def check(rc: int, what: str):
 KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_fwd": 3,
               "k_composite_bwd": 4, "k_mlp_dx": 5, "k_param_reduce": 6, "k_ray_grads": 7,
               "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10,
-              "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14}
+              "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15}
 
 
 class KernelTimer:

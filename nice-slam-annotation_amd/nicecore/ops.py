@@ -11,30 +11,35 @@ def _grid_args(c):
     return [c.get(k) if c is not None else None for k in L.GRID_KEYS]
 
 
-def eval_points(decoders, p, c_grid, stage='middle'):
+def eval_points(decoders, p, c_grid, stage='middle', deterministic=None):
     """NICE.forward(p, c_grid, stage) (src/conv_onet/models/decoder.py:336-370):
     raw [P,4] float32 for points p ([P,3] or [1,P,3]); differentiable w.r.t. p,
-    the grids and the decoder parameters."""
+    the grids and the decoder parameters.  ``deterministic``: see render_rays."""
     plan = make_plan(stage, decoders)
-    spec = {"plan": plan}
+    spec = {"plan": plan, "deterministic": deterministic}
     return NiceEvalFn.apply(spec, p, *_grid_args(c_grid), *plan.flat_params())
 
 
 def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_strat=32,
-                n_surf=16, depth_max=None):
+                n_surf=16, depth_max=None, deterministic=None):
     """Renderer.render_batch_ray core (src/utils/Renderer.py:95-262) with
     N_importance = 0, lindisp = False, perturb = 0, occupancy = True.
     Returns (depth float64 [N], uncertainty float64 [N], color float32 [N,3]).
 
     ``depth_max``: optional device scalar replacing the batch-global max(gt_depth)
-    (Renderer.py:157, :194) -- pass the all-reduced max when a batch is sharded."""
+    (Renderer.py:157, :194) -- pass the all-reduced max when a batch is sharded.
+
+    ``deterministic``: grid gradients by an ordered per-voxel reduction (bit-identical
+    run to run) instead of float atomics; None = the environment variable
+    ``NC_DETERMINISTIC=1`` or ``torch.use_deterministic_algorithms(True)``."""
     if stage == 'coarse':
         gt_depth = None
     ns = n_surf if gt_depth is not None else 0
     if n_strat + ns > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
         raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
-    spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max}
+    spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
+            "deterministic": deterministic}
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
 
 
@@ -43,7 +48,7 @@ _LOSS_KINDS = {"mapper": L.NC_LOSS_MAPPER, "tracker": L.NC_LOSS_TRACKER}
 
 def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, loss="mapper",
                      target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
-                     gt_depth="target", n_strat=32, n_surf=16, depth_max=None):
+                     gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None):
     """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
     color, loss) with ``loss`` a float64 device scalar that backpropagates into the
     grids / decoders / rays like the reference's loss expression:
@@ -75,6 +80,6 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
         raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
-            "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth,
+            "deterministic": deterministic, "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth,
                      target_color if color_term else None)}
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())

@@ -15,6 +15,7 @@ gradient and grid scatter).
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 
 import torch
@@ -46,6 +47,22 @@ def _bound_rows(b) -> list:
         return rows
     t = torch.as_tensor(b, dtype=torch.float64).reshape(3, 2)
     return [[float(t[k, 0]), float(t[k, 1])] for k in range(3)]
+
+
+def deterministic_requested(spec=None) -> bool:
+    """NC_DETERMINISTIC (ordered grid-gradient reduction instead of float atomics):
+    asked for by ``spec["deterministic"]``, else by the environment variable
+    ``NC_DETERMINISTIC=1`` or ``torch.use_deterministic_algorithms(True)``."""
+    d = spec.get("deterministic") if spec else None
+    if d is not None:
+        return bool(d)
+    return os.environ.get("NC_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
+
+
+def _flags(ctx, spec):
+    if not any(ctx.needs_input_grad):
+        return 0
+    return L.NC_SAVE_FOR_BACKWARD | (L.NC_DETERMINISTIC if deterministic_requested(spec) else 0)
 
 
 def decoder_modules(decoders):
@@ -317,7 +334,7 @@ class NiceRenderFn(torch.autograd.Function):
         N = rays_o.shape[0]
         a = L.NcRenderArgs.from_buffer_copy(
             plan.render_template(device, spec["n_strat"], spec["n_surf"], spec["bound"]))
-        a.flags = L.NC_SAVE_FOR_BACKWARD if any(ctx.needs_input_grad) else 0
+        a.flags = _flags(ctx, spec)
         a.n_rays = N
         a.rays_o = rays_o.data_ptr()
         a.rays_d = rays_d.data_ptr()
@@ -408,7 +425,7 @@ class NiceEvalFn(torch.autograd.Function):
         P = pts.shape[0]
         a = L.NcPointsArgs.from_buffer_copy(plan.points_template(device))
         a.n_points = P
-        a.flags = L.NC_SAVE_FOR_BACKWARD if any(ctx.needs_input_grad) else 0
+        a.flags = _flags(ctx, spec)
         a.pts = pts.data_ptr()
         grids = (g0, g1, g2, g3)
         gkeep = []

@@ -1,0 +1,115 @@
+"""NC_DETERMINISTIC (SURVEY.md §8b "Determinism") and non-leaf feature grids
+(the Mapper's frustum mode builds each grid as ``val[mask] =
+val_grad``, Mapper.py:492-500, so the core's dense grid gradient must compose with
+autograd's index_put backward).
+
+Deterministic mode replaces the grid-gradient float atomics with an ordered
+per-voxel reduction (nc_det.hip).  Checks: two runs are bit-identical; the result
+matches the golden reference vectors at the same tolerance as the atomic path; and
+it agrees with the atomic path to float32 reassociation (1e-5 of max-abs)."""
+import pytest
+import torch
+
+from conftest import CASE_NAMES, load_case, load_scene
+from parity_common import build_model, case_stage, make_renderer, rel_err, run_case
+from test_gpu_parity import GRAD_TOL, _assert_case, _room0_case
+
+
+def _render_grads(sc, grids, params, ro, rd, dep, stage, deterministic, seed=11):
+    from nicecore.ops import render_rays
+    model = build_model(params, sc.bound, sc.bound * 2, "cuda")
+    g_g = {k: v.cuda().contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+           for k, v in grids.items()}
+    ro_g, rd_g = ro.cuda().requires_grad_(True), rd.cuda().requires_grad_(True)
+    gt = dep.cuda() if stage != "coarse" else None
+    d, u, c = render_rays(model, g_g, ro_g, rd_g, sc.bound, stage, gt, deterministic=deterministic)
+    gen = torch.Generator().manual_seed(seed)
+    up = [torch.randn(d.shape, generator=gen, dtype=torch.float64).cuda(),
+          torch.randn(u.shape, generator=gen, dtype=torch.float64).cuda(),
+          torch.randn(c.shape, generator=gen).cuda()]
+    torch.autograd.backward([d, u, c], up)
+    out = {"grad/rays_o": ro_g.grad, "grad/rays_d": rd_g.grad}
+    for k, v in g_g.items():
+        if v.grad is not None:
+            out["grad/" + k] = v.grad
+    for n, p in model.named_parameters():
+        if p.grad is not None:
+            out["grad/param/" + n] = p.grad
+    return {k: v.detach().cpu() for k, v in out.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stage", ["color", "middle", "coarse"])
+def test_deterministic_bitwise_repeatable(stage):
+    sc, grids, params, ro, rd, dep = _room0_case(512, stage, seed=21)
+    a = _render_grads(sc, grids, params, ro, rd, dep, stage, True)
+    b = _render_grads(sc, grids, params, ro, rd, dep, stage, True)
+    assert a.keys() == b.keys() and any(k.startswith("grad/grid") for k in a)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    # same gradients as the atomic path up to float32 reassociation
+    c = _render_grads(sc, grids, params, ro, rd, dep, stage, False)
+    for k in a:
+        assert rel_err(a[k], c[k]) <= 1e-5, (k, rel_err(a[k], c[k]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASE_NAMES)
+def test_deterministic_matches_reference(case, monkeypatch):
+    """Golden vectors through the deterministic path (env switch, as a user sets it)."""
+    monkeypatch.setenv("NC_DETERMINISTIC", "1")
+    rec, got = run_case(case, channels_last=True)
+    _assert_case(rec, got)
+
+
+@pytest.mark.gpu
+def test_deterministic_via_torch_switch():
+    from nicecore.render_fn import deterministic_requested
+    old = torch.are_deterministic_algorithms_enabled()
+    try:
+        torch.use_deterministic_algorithms(True)
+        assert deterministic_requested({})
+        assert not deterministic_requested({"deterministic": False})
+    finally:
+        torch.use_deterministic_algorithms(old)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_frustum_masked_nonleaf_grids(deterministic):
+    """Mapper frustum mode (Mapper.py:393-404, :492-500): the optimised leaves are
+    val_grad = grid[mask]; the rendered grid is a non-leaf built by index_put.  The
+    leaves' gradient must equal the dense grid gradient at the mask."""
+    bound, cbound, grids, params = load_scene()
+    rec = load_case("color_depth")
+    stage, _ = case_stage("color_depth")
+    model = build_model(params, bound, cbound, "cuda")
+    r = make_renderer(bound)
+    gen = torch.Generator().manual_seed(4)
+    # dense reference: leaf grids
+    dense = {k: v.cuda().requires_grad_(True) for k, v in grids.items()}
+    d, u, c = r.render_batch_ray(dense, model, rec["rays_d"].cuda(), rec["rays_o"].cuda(), "cuda", stage,
+                                 rec["gt_depth"].cuda())
+    torch.autograd.backward([d, u, c], [rec["g_depth"].cuda(), rec["g_var"].cuda(), rec["g_color"].cuda()])
+    # frustum mode: mask over the voxels (every channel), leaf = masked values
+    leaves, built = {}, {}
+    for k, v in grids.items():
+        m = torch.rand(v.shape[2:], generator=gen) < 0.6
+        mask = m[None, None].expand_as(v).cuda()
+        val = v.clone().cuda()
+        val_grad = v.cuda()[mask].clone().requires_grad_(True)
+        val[mask] = val_grad  # Mapper.py:495-500
+        leaves[k] = (val_grad, mask)
+        built[k] = val
+    from nicecore.ops import render_rays
+    d2, u2, c2 = render_rays(model, built, rec["rays_o"].cuda(), rec["rays_d"].cuda(), bound, stage,
+                             rec["gt_depth"].cuda(), deterministic=deterministic)
+    assert torch.equal(d2, d) and torch.equal(c2, c)
+    torch.autograd.backward([d2, u2, c2], [rec["g_depth"].cuda(), rec["g_var"].cuda(), rec["g_color"].cuda()])
+    for k, (vg, mask) in leaves.items():
+        ref = dense[k].grad
+        if ref is None:
+            assert vg.grad is None or float(vg.grad.abs().max()) == 0.0
+            continue
+        assert vg.grad is not None, k
+        assert rel_err(vg.grad.cpu(), ref[mask].cpu()) <= GRAD_TOL, k
