@@ -15,6 +15,11 @@
  *                       the four feature grids and every decoder parameter.
  *   nc_points_forward   src/conv_onet/models/decoder.py:336-370 NICE.forward on
  *   nc_points_backward  caller-given points (Renderer.eval_points / Mesher use).
+ *   nc_sample_rays_*    src/common.py:74-137 get_samples / get_rays_from_uv over a
+ *                       batch of frames + the Tracker/Mapper bbox pre-filter, and the
+ *                       pose gradient (Tracker.py:95-111, Mapper.py:543-591).
+ *   nc_frustum_mask     src/Mapper.py:100-187 get_mask_from_c2w (frustum feature
+ *                       selection of one grid).
  *
  * Conventions
  *   - All pointers are device pointers on the current HIP device; the library
@@ -42,7 +47,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 3
+#define NC_ABI_VERSION 4
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -150,6 +155,85 @@ typedef struct nc_points_args {
   double* g_pts;           /* [P,3] or NULL */
 } nc_points_args;
 
+/* Training-ray sampling of one or more camera frames (ABI v4).  Replaces, in one
+ * launch over all frames of an iteration:
+ *   src/common.py:74-89   get_rays_from_uv (dirs = ((i-cx)/fx, -(j-cy)/fy, -1),
+ *                         rays_d = sum(dirs * c2w[:3,:3], -1), rays_o = c2w[:3,3])
+ *   src/common.py:92-108  select_uv (gather of the chosen pixels' depth / colour)
+ *   src/common.py:111-137 get_sample_uv / get_samples (region H0..H1 x W0..W1; pixel
+ *                         k of the region is (i, j) = (W0 + k % (W1-W0), H0 + k / (W1-W0)))
+ *   src/Tracker.py:100-107, src/Mapper.py:580-591  the bbox pre-filter
+ *                         inside = min_axis max_side (bound - o) / d >= gt_depth
+ *                         (float64, NaN -> outside)
+ * The caller draws the pixel indices (torch.randint, as select_uv does) and, when
+ * the reference compacts the batch with `inside`, does that itself.  Backward:
+ * d c2w[f] (rows 0..2: d R | d t) from d rays_o / d rays_d, summed over the frame's
+ * rays in a fixed order. */
+#define NC_POSE_F32 0
+#define NC_POSE_F64 1
+typedef struct nc_sample_args {
+  int32_t abi_version;
+  int32_t pose_dtype;        /* NC_POSE_F32 / NC_POSE_F64 (the c2w tensor's dtype) */
+  int64_t n_frames;          /* F */
+  int64_t n_per_frame;       /* n rays drawn per frame */
+  int64_t H0, H1, W0, W1;    /* sampling region (get_samples' arguments) */
+  float fx, fy, cx, cy;      /* intrinsics, as the float32 scalars torch applies them */
+  const void* c2w;           /* [F] camera-to-world poses, rows 0..2 used */
+  int64_t c2w_stride[3];     /* frame, row, column strides (elements) */
+  const int64_t* indices;    /* [F][n] flat index into the region, row-major */
+  const float* pix_i;        /* optional [F][n] float pixel columns / rows instead of indices */
+  const float* pix_j;        /*   (get_rays_from_uv on caller uv; no depth / colour gather) */
+  const int64_t* frame_ids;  /* optional [F]: image slot of pose f in depth / color (a resident
+                                keyframe image stack); NULL = slot f */
+  const float* depth;        /* [K] depth images [H][W], NULL = no depth output */
+  int64_t depth_stride[3];   /* frame, row, column */
+  const float* color;        /* [K] colour images [H][W][3], NULL = no colour output */
+  int64_t color_stride[4];   /* frame, row, column, channel */
+  const double* bound;       /* [3][2] scene bound for the pre-filter, or NULL */
+  /* forward outputs ([F*n] rows, frame-major; rays in the pose dtype) */
+  void* rays_o;              /* [F*n][3] */
+  void* rays_d;              /* [F*n][3] */
+  float* gt_depth;           /* [F*n] (needs depth) */
+  float* gt_color;           /* [F*n][3] (needs color) */
+  uint8_t* inside;           /* [F*n] bbox pre-filter mask (needs bound and depth) */
+  /* backward */
+  const void* g_rays_o;      /* [F*n][3] pose dtype, NULL = 0 */
+  const void* g_rays_d;      /* [F*n][3] pose dtype, NULL = 0 */
+  void* g_c2w;               /* [F][3][4] contiguous, pose dtype (written) */
+} nc_sample_args;
+
+int nc_sample_rays_forward(const nc_sample_args* args, void* stream);
+int nc_sample_rays_backward(const nc_sample_args* args, void* stream);
+
+/* Frustum feature selection (ABI v4): Mapper.get_mask_from_c2w (src/Mapper.py:100-187)
+ * for one grid on the device.  Per voxel (x, y, z) with world point (xs[x], ys[y],
+ * zs[z]) -- the caller's torch.linspace tables, as the reference builds them --
+ *   cam = w2c @ [p, 1] (float32), cam.x *= -1, uv = K @ cam (float64), z = uv.z + 1e-5,
+ *   (u, v) = float32(uv.xy / z), d = cv2.remap(depth, u, v, INTER_LINEAR) (OpenCV 4.5:
+ *   5-bit fixed-point sub-pixel weights, constant-0 border), d == 0 -> max over all d,
+ *   mask = 0 < u < W & 0 < v < H & 0 <= -z <= d + 0.5  |  |p - c2w[:3,3]|^2 < 0.25.
+ * Output in the grid's own [D][H][W] = [z][y][x] order (the reference returns the
+ * [x][y][z] transpose, Mapper.py:185, and permutes it back at :394). */
+typedef struct nc_frustum_args {
+  int32_t abi_version;
+  int32_t reserved;
+  int64_t nx, ny, nz;          /* grid size along x, y, z (val_shape[2], [1], [0]) */
+  const float* xs;             /* [nx] world x of the voxel columns (torch.linspace, float32) */
+  const float* ys;             /* [ny] */
+  const float* zs;             /* [nz] */
+  float w2c[16];               /* np.linalg.inv(c2w) in float32, row-major 4x4 */
+  float cam_o[3];              /* c2w[:3, 3] (float32) */
+  float reserved2;
+  double fx, fy, cx, cy;       /* intrinsics (float64, numpy's K) */
+  const float* depth;          /* [H][W] float32 depth image */
+  int64_t H, W;
+  int64_t depth_stride[2];     /* row, column (elements) */
+  uint8_t* mask;               /* [nz][ny][nx] output (bool) */
+  uint32_t* scratch;           /* one uint32 of device scratch (max depth) */
+} nc_frustum_args;
+
+int nc_frustum_mask(const nc_frustum_args* args, void* stream);
+
 int nc_abi_version(void);
 const char* nc_last_error(void);
 
@@ -157,7 +241,7 @@ const char* nc_last_error(void);
 int64_t nc_param_count(int decoder);
 
 /* sizeof() of the ABI structs, for binding-layout checks:
- * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params. */
+ * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params, 4 nc_sample_args, 5 nc_frustum_args. */
 size_t nc_struct_size(int which);
 
 size_t nc_render_workspace_bytes(const nc_render_args* args);

@@ -36,12 +36,13 @@ int check_hip(int e, const char* what) {
 enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
-  KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_COUNT
+  KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
-                                       "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter"};
+                                       "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
+                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -472,6 +473,8 @@ size_t nc_struct_size(int which) {
     case 1: return sizeof(nc_points_args);
     case 2: return sizeof(nc_grid);
     case 3: return sizeof(nc_decoder_params);
+    case 4: return sizeof(nc_sample_args);
+    case 5: return sizeof(nc_frustum_args);
   }
   return 0;
 }
@@ -600,6 +603,48 @@ int nc_points_backward(const nc_points_args* a, void* ws, size_t ws_bytes, void*
   if (a->g_pts)
     if (int e = check_hip(timed(KID_POINTS_GRADS, s, [&] { return launch_points_grads(m, a->g_pts, s); }), "k_points_grads")) return e;
   return 0;
+}
+
+static int sample_check(const nc_sample_args* a) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (a->pose_dtype != NC_POSE_F32 && a->pose_dtype != NC_POSE_F64) return fail(-1, "nicecore: unknown pose dtype");
+  if (a->n_frames < 0 || a->n_per_frame < 0) return fail(-1, "nicecore: negative frame / ray count");
+  if (a->H0 < 0 || a->W0 < 0 || a->H1 <= a->H0 || a->W1 <= a->W0) return fail(-1, "nicecore: empty sampling region");
+  if (a->n_frames * a->n_per_frame > 0 && (!a->c2w || (!a->indices && !(a->pix_i && a->pix_j))))
+    return fail(-1, "nicecore: sampling needs c2w and indices (or pix_i and pix_j)");
+  if (a->pix_i && (a->depth || a->color)) return fail(-1, "nicecore: pix_i / pix_j rays gather no depth or colour");
+  return 0;
+}
+
+int nc_sample_rays_forward(const nc_sample_args* a, void* stream) {
+  if (int e = sample_check(a)) return e;
+  if (a->n_frames * a->n_per_frame == 0) return 0;
+  if (!a->rays_o || !a->rays_d) return fail(-1, "nicecore: NULL ray outputs");
+  if ((a->depth && !a->gt_depth) || (a->color && !a->gt_color)) return fail(-1, "nicecore: NULL depth / colour output");
+  if (a->inside && (!a->bound || !a->depth)) return fail(-1, "nicecore: the bbox pre-filter needs bound and depth");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_SAMPLE_RAYS, s, [&] { return launch_sample_rays(*a, s); }), "k_sample_rays");
+}
+
+int nc_sample_rays_backward(const nc_sample_args* a, void* stream) {
+  if (int e = sample_check(a)) return e;
+  if (a->n_frames == 0) return 0;
+  if (!a->g_c2w) return fail(-1, "nicecore: NULL pose gradient output");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_SAMPLE_POSE_GRAD, s, [&] { return launch_sample_pose_grad(*a, s); }), "k_sample_pose_grad");
+}
+
+int nc_frustum_mask(const nc_frustum_args* a, void* stream) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (a->nx < 0 || a->ny < 0 || a->nz < 0 || a->H < 1 || a->W < 1) return fail(-1, "nicecore: bad grid or image size");
+  if (a->nx * a->ny * a->nz == 0) return 0;
+  if (!a->xs || !a->ys || !a->zs || !a->depth || !a->mask || !a->scratch)
+    return fail(-1, "nicecore: NULL frustum input or output");
+  if (a->H > 32767 || a->W > 32767) return fail(-1, "nicecore: cv2.remap semantics need H, W < 32768");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_FRUSTUM, s, [&] { return launch_frustum_mask(*a, s); }), "k_frustum_mask");
 }
 
 }  // extern "C"

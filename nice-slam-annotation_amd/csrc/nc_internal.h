@@ -68,6 +68,12 @@ struct DetBufs {
 size_t det_sort_temp_bytes(int64_t n_entries, int end_bit);
 int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s);
 
+// training-ray sampling (nc_sample.hip)
+int launch_sample_rays(const nc_sample_args& a, hipStream_t s);
+int launch_sample_pose_grad(const nc_sample_args& a, hipStream_t s);
+// frustum feature selection (nc_frustum.hip)
+int launch_frustum_mask(const nc_frustum_args& a, hipStream_t s);
+
 // Arguments of the per-ray kernels (sampling, compositing, ray gradients).
 struct RayCtx {
   int64_t N;

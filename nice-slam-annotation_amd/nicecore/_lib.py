@@ -12,7 +12,7 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 3
+NC_ABI_VERSION = 4
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
 NC_LOSS_NONE, NC_LOSS_MAPPER, NC_LOSS_TRACKER = 0, 1, 2
@@ -62,6 +62,30 @@ class NcPointsArgs(ctypes.Structure):
                 ("raw", c_void_p), ("g_raw", c_void_p), ("g_pts", c_void_p)]
 
 
+NC_POSE_F32, NC_POSE_F64 = 0, 1
+
+
+class NcSampleArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("pose_dtype", c_int32), ("n_frames", c_int64),
+                ("n_per_frame", c_int64), ("H0", c_int64), ("H1", c_int64), ("W0", c_int64),
+                ("W1", c_int64), ("fx", c_float), ("fy", c_float), ("cx", c_float), ("cy", c_float),
+                ("c2w", c_void_p), ("c2w_stride", c_int64 * 3), ("indices", c_void_p),
+                ("pix_i", c_void_p), ("pix_j", c_void_p), ("frame_ids", c_void_p), ("depth", c_void_p), ("depth_stride", c_int64 * 3), ("color", c_void_p),
+                ("color_stride", c_int64 * 4), ("bound", c_void_p), ("rays_o", c_void_p),
+                ("rays_d", c_void_p), ("gt_depth", c_void_p), ("gt_color", c_void_p),
+                ("inside", c_void_p), ("g_rays_o", c_void_p), ("g_rays_d", c_void_p),
+                ("g_c2w", c_void_p)]
+
+
+class NcFrustumArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("reserved", c_int32), ("nx", c_int64), ("ny", c_int64),
+                ("nz", c_int64), ("xs", c_void_p), ("ys", c_void_p), ("zs", c_void_p),
+                ("w2c", c_float * 16), ("cam_o", c_float * 3), ("reserved2", c_float),
+                ("fx", c_double), ("fy", c_double), ("cx", c_double), ("cy", c_double),
+                ("depth", c_void_p), ("H", c_int64), ("W", c_int64), ("depth_stride", c_int64 * 2),
+                ("mask", c_void_p), ("scratch", c_void_p)]
+
+
 EXPORTS = {
     "nc_abi_version": (c_int, []),
     "nc_last_error": (ctypes.c_char_p, []),
@@ -76,6 +100,9 @@ EXPORTS = {
     "nc_points_workspace_bytes": (c_size_t, [POINTER(NcPointsArgs)]),
     "nc_points_forward": (c_int, [POINTER(NcPointsArgs), c_void_p, c_size_t, c_void_p]),
     "nc_points_backward": (c_int, [POINTER(NcPointsArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_sample_rays_forward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
+    "nc_sample_rays_backward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
+    "nc_frustum_mask": (c_int, [POINTER(NcFrustumArgs), c_void_p]),
 }
 
 _lib = None
@@ -115,7 +142,8 @@ def check(rc: int, what: str):
 KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_fwd": 3,
               "k_composite_bwd": 4, "k_mlp_dx": 5, "k_param_reduce": 6, "k_ray_grads": 7,
               "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10,
-              "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15}
+              "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15,
+              "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18}
 
 
 class KernelTimer:
@@ -134,7 +162,7 @@ class KernelTimer:
 
     def __exit__(self, *exc):
         lib = load()
-        n = 16
+        n = 32
         ms = (c_double * n)()
         cnt = (c_int64 * n)()
         k = lib.nc_timing_stop(ms, cnt, n)

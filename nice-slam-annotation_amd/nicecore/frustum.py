@@ -1,0 +1,84 @@
+"""Frustum feature selection on the HIP core (ABI v4, nc_frustum_mask).
+
+``FrustumSelector.get_mask_from_c2w(c2w, key, val_shape, depth_np)`` has the signature
+and result of ``Mapper.get_mask_from_c2w`` (src/Mapper.py:100-187): a bool mask
+[X, Y, Z] of the grid voxels inside the camera frustum (depth-tested against the
+frame's depth image) or within 0.5 m of the camera centre.  Here the mask is a device
+tensor (a permuted view of the kernel's [Z, Y, X] output, so ``.permute(2, 1, 0)`` as
+the Mapper does at :394 gives back the contiguous grid-order mask), and the per-voxel
+work -- projection, cv2.remap of the depth image, depth test -- runs as two kernels
+instead of numpy + OpenCV over every voxel on the host.
+
+Host-side, exactly as the reference: the voxel coordinate tables (torch.linspace on
+the CPU, cached per bound and shape) and w2c = np.linalg.inv(c2w) in float32.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+class FrustumSelector:
+    def __init__(self, bound, H, W, fx, fy, cx, cy, device="cuda"):
+        self.bound = bound
+        self.H, self.W, self.fx, self.fy, self.cx, self.cy = H, W, fx, fy, cx, cy
+        self.device = torch.device(device)
+        self._tables = {}
+        self._scratch = None
+
+    def _axis_tables(self, val_shape):
+        key = tuple(int(s) for s in val_shape)
+        t = self._tables.get(key)
+        if t is None:
+            b = self.bound
+            t = (torch.linspace(b[0][0], b[0][1], key[2]).to(self.device),   # Mapper.py:116-118
+                 torch.linspace(b[1][0], b[1][1], key[1]).to(self.device),
+                 torch.linspace(b[2][0], b[2][1], key[0]).to(self.device))
+            self._tables[key] = t
+        return t
+
+    def grid_mask(self, c2w, key, val_shape, depth):
+        """The mask in the grid's own [Z, Y, X] order (bool, device)."""
+        val_shape = tuple(int(s) for s in val_shape)
+        if key == 'grid_coarse':  # Mapper.py:121-123
+            return torch.ones(val_shape, dtype=torch.bool, device=self.device)
+        lib = L.load()
+        if self.device.type != "cuda":
+            raise L.NiceCoreError("nicecore selects frustum features on a HIP device")
+        xs, ys, zs = self._axis_tables(val_shape)
+        c2w_np = c2w.detach().cpu().numpy() if isinstance(c2w, torch.Tensor) else np.asarray(c2w)
+        w2c = np.linalg.inv(c2w_np)  # Mapper.py:126, in c2w's dtype
+        depth_t = torch.as_tensor(depth).to(self.device, torch.float32)
+        if depth_t.dim() != 2:
+            raise L.NiceCoreError("depth must be an [H, W] image")
+        a = L.NcFrustumArgs()
+        a.abi_version = L.NC_ABI_VERSION
+        a.nx, a.ny, a.nz = val_shape[2], val_shape[1], val_shape[0]
+        a.xs, a.ys, a.zs = xs.data_ptr(), ys.data_ptr(), zs.data_ptr()
+        w = w2c.astype(np.float32).reshape(-1)
+        for k in range(16):
+            a.w2c[k] = float(w[k])
+        o = c2w_np[:3, 3].astype(np.float32)
+        for k in range(3):
+            a.cam_o[k] = float(o[k])
+        a.fx, a.fy, a.cx, a.cy = float(self.fx), float(self.fy), float(self.cx), float(self.cy)
+        a.depth = depth_t.data_ptr()
+        a.H, a.W = depth_t.shape
+        a.depth_stride[0], a.depth_stride[1] = depth_t.stride()
+        mask = torch.empty(val_shape, dtype=torch.bool, device=self.device)
+        if self._scratch is None:
+            self._scratch = torch.zeros(1, dtype=torch.int32, device=self.device)
+        a.mask = mask.data_ptr()
+        a.scratch = self._scratch.data_ptr()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        L.check(lib.nc_frustum_mask(ctypes.byref(a), stream), "nc_frustum_mask")
+        self._keep = depth_t
+        return mask
+
+    def get_mask_from_c2w(self, c2w, key, val_shape, depth_np):
+        """Mapper.py:100-187: bool mask [X, Y, Z] (device tensor view)."""
+        return self.grid_mask(c2w, key, val_shape, depth_np).permute(2, 1, 0)

@@ -39,6 +39,8 @@ def test_struct_layouts_match(lib):
     assert lib.nc_struct_size(1) == ctypes.sizeof(L.NcPointsArgs)
     assert lib.nc_struct_size(2) == ctypes.sizeof(L.NcGrid)
     assert lib.nc_struct_size(3) == ctypes.sizeof(L.NcDecoderParams)
+    assert lib.nc_struct_size(4) == ctypes.sizeof(L.NcSampleArgs)
+    assert lib.nc_struct_size(5) == ctypes.sizeof(L.NcFrustumArgs)
     assert lib.nc_abi_version() == L.NC_ABI_VERSION
 
 
@@ -88,3 +90,29 @@ def test_loss_args_validated(lib):
         a = args(**kw)
         assert lib.nc_render_workspace_bytes(ctypes.byref(a)) == 0, kw
         assert msg in lib.nc_last_error(), (kw, lib.nc_last_error())
+
+
+def test_sample_args_validated(lib):
+    """nc_sample_rays_* (ABI v4) reject bad arguments before any launch."""
+    a = L.NcSampleArgs()
+    a.abi_version = L.NC_ABI_VERSION
+    a.n_frames, a.n_per_frame = 1, 4
+    a.H0, a.H1, a.W0, a.W1 = 0, 4, 0, 4
+    a.pose_dtype = 3
+    assert lib.nc_sample_rays_forward(ctypes.byref(a), None) < 0
+    assert b"pose dtype" in lib.nc_last_error()
+    a.pose_dtype = L.NC_POSE_F32
+    a.H1 = 0
+    assert lib.nc_sample_rays_forward(ctypes.byref(a), None) < 0
+    assert b"region" in lib.nc_last_error()
+    a.H1 = 4
+    assert lib.nc_sample_rays_forward(ctypes.byref(a), None) < 0
+    assert b"c2w and indices" in lib.nc_last_error()
+    a.c2w, a.indices = 8, 8
+    assert lib.nc_sample_rays_forward(ctypes.byref(a), None) < 0
+    assert b"ray outputs" in lib.nc_last_error()
+    a.rays_o, a.rays_d, a.inside = 8, 8, 8
+    assert lib.nc_sample_rays_forward(ctypes.byref(a), None) < 0
+    assert b"pre-filter" in lib.nc_last_error()
+    assert lib.nc_sample_rays_backward(ctypes.byref(a), None) < 0
+    assert b"pose gradient" in lib.nc_last_error()
