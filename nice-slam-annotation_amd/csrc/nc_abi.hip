@@ -152,9 +152,29 @@ struct Ws {
   int vbits = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
-  int slab_wgs = 1;
+  int slab_wgs = 1;        // total k_mlp_dw workgroups (= slab rows)
+  int32_t dw_off[MAX_JOBS + 1] = {0, 0, 0, 0};
   int64_t slab_stride = 0;
 };
+
+// Split `total` resident workgroups over the jobs in proportion to their per-point
+// cost (decoder MACs), each job at least 1 and at most its `blocks` work items;
+// off[j]..off[j+1] are job j's workgroups of a 1-D grid, off[k > n_jobs] = off[n_jobs].
+void split_wgs(int total, int64_t blocks, const Job* jobs, int n_jobs, int32_t* off) {
+  if (total < n_jobs) total = n_jobs;
+  int64_t wsum = 0;
+  for (int j = 0; j < n_jobs; ++j) wsum += decoder_macs(jobs[j].kind);
+  off[0] = 0;
+  int64_t acc = 0;
+  for (int j = 0; j < n_jobs; ++j) {
+    acc += decoder_macs(jobs[j].kind);
+    int64_t n = (total * acc + wsum / 2) / wsum - off[j];  // rounded cumulative share
+    if (n < 1) n = 1;
+    if (n > blocks) n = blocks > 0 ? blocks : 1;
+    off[j + 1] = off[j] + (int32_t)n;
+  }
+  for (int j = n_jobs + 1; j <= MAX_JOBS; ++j) off[j] = off[n_jobs];
+}
 
 void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1) {
   size_t off = 0;
@@ -195,12 +215,11 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
   }
   const int64_t blocks = (P + 31) / 32;  // k_mlp_dw sub-chunks
   // one wave of resident workgroups over all jobs (floor: a 257th workgroup on a
-  // 256-CU chip would run as a second, serial round)
-  int per_job = cu_count() * mlp_blocks_per_cu(2) / pl.n_jobs;
-  if (per_job < 1) per_job = 1;
-  w.slab_wgs = (int)((blocks < per_job) ? (blocks > 0 ? blocks : 1) : per_job);
+  // 256-CU chip would run as a second, serial round), split by the decoders' cost
+  split_wgs(cu_count() * mlp_blocks_per_cu(2), blocks, pl.jobs, pl.n_jobs, w.dw_off);
+  w.slab_wgs = w.dw_off[pl.n_jobs];
   w.slab_stride = (max_param_count() + 63) & ~int64_t(63);
-  w.slab = take((size_t)pl.n_jobs * w.slab_wgs * w.slab_stride * 4);
+  w.slab = take((size_t)w.slab_wgs * w.slab_stride * 4);
   if (save && vbits > 0) {  // NC_DETERMINISTIC grid-gradient buffers (nc_det.hip)
     const int64_t ne = (int64_t)pl.n_jobs * P * 8;
     w.det = true;
@@ -229,6 +248,11 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.n_jobs = pl.n_jobs;
   m.slab_wgs = w.slab_wgs;
   m.slab_stride = w.slab_stride;
+  std::memcpy(m.dw_off, w.dw_off, sizeof(m.dw_off));
+  {  // k_mlp_fwd split: one wave of resident workgroups, 16-point tiles per wave
+    const int64_t per = FWD_THREADS / 64 * 16 * FWD_TILES;
+    split_wgs(cu_count() * mlp_blocks_per_cu(0), (P + per - 1) / per, pl.jobs, pl.n_jobs, m.fwd_off);
+  }
   m.save_rec = w.save;
   for (int j = 0; j < pl.n_jobs; ++j) {
     m.jobs[j] = pl.jobs[j];
@@ -417,6 +441,7 @@ int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s) 
   r.slab_wgs = m.slab_wgs;
   r.slab_stride = m.slab_stride;
   r.slab = m.slab;
+  std::memcpy(r.wg_off, m.dw_off, sizeof(r.wg_off));
   bool any = false;
   for (int j = 0; j < m.n_jobs; ++j) {
     r.jobs[j] = m.jobs[j];
@@ -511,7 +536,7 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
   if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
-  if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(P, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
+  if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
   if (int e = check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd")) return e;
   if (a->loss != NC_LOSS_NONE)
     if (int e = check_hip(timed(KID_LOSS, s, [&] { return launch_loss(rc, s); }), "k_loss")) return e;
@@ -581,7 +606,7 @@ int nc_points_forward(const nc_points_args* a, void* ws, size_t ws_bytes, void* 
   fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, false);
   if (int e = check_hip(launch_points_prep(m, (float4*)m.xyz, (float4*)m.pf, s), "k_points_prep")) return e;
   if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
-  if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, fwd_grid_x(a->n_points, pl.n_jobs), s); }), "k_mlp_fwd")) return e;
+  if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
   return check_hip(timed(KID_POINTS_ASSEMBLE, s, [&] { return launch_points_assemble(m, a->stage, a->raw, s); }), "k_points_assemble");
 }
 

@@ -48,6 +48,9 @@ struct MlpCtx {
                              // by backward activations (k_mlp_dx); both read by k_mlp_dw
   float* slab;               // [n_jobs][slab_wgs][slab_stride] per-workgroup parameter gradients
   int64_t slab_stride;
+  int32_t fwd_off[MAX_JOBS + 1];  // k_mlp_fwd: workgroups [off[j], off[j+1]) of the 1-D grid run job j
+  int32_t dw_off[MAX_JOBS + 1];   // k_mlp_dw: same, and slab row = workgroup index
+                                  // (both split in proportion to the decoders' per-point MACs)
   float* dfeat;              // NC_DETERMINISTIC: [n_jobs][P][32] d features of each job's own grid
                              // (k_mlp_dx stores them instead of scattering with atomics), else NULL
 };
@@ -123,6 +126,7 @@ struct RayCtx {
 struct ParamReduceCtx {
   int32_t n_jobs;
   int32_t slab_wgs;
+  int32_t wg_off[MAX_JOBS + 1];  // job j's slab rows [wg_off[j], wg_off[j+1])
   int64_t slab_stride;
   Job jobs[MAX_JOBS];
   float* grad[MAX_JOBS];
@@ -149,7 +153,8 @@ int mlp_dw_lds_bytes();
 int mlp_dx_lds_bytes();
 int mlp_blocks_per_cu(int which);  // 0 k_mlp_fwd, 1 k_mlp_dx, 2 k_mlp_dw
 int rec_stride(int kind);  // floats per point of a decoder's [forward | backward] record
-int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s);
+int launch_mlp_fwd(const MlpCtx& c, hipStream_t s);  // grid = c.fwd_off[n_jobs]
+int decoder_macs(int kind);  // multiply-adds per point of one decoder's forward
 int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dw(const MlpCtx& c, hipStream_t s);
 int launch_grid_gather(const MlpCtx& c, hipStream_t s);

@@ -40,42 +40,97 @@ namespace nc {
 
 // ---------------------------------------------------------------------------
 // weights: nn.Parameter storage -> LDS image (layout: Net<KIND>)
+// Every thread first issues ALL of its global loads (one register array per
+// parameter tensor, compile-time trip counts for the NT-thread workgroup), then
+// zero-fills the padding of the image and stores: one memory round trip for the
+// whole prologue instead of one per tensor.
 // ---------------------------------------------------------------------------
-template <int KIND, int PADW>
+template <int CNT, int NT>
+struct SegRegs {
+  static constexpr int PER = (CNT + NT - 1) / NT;
+  float v[PER];
+  __device__ __forceinline__ void load(const float* src) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = (int)threadIdx.x + k * NT;
+      v[k] = (e < CNT) ? src[e] : 0.f;
+    }
+  }
+  template <typename F>
+  __device__ __forceinline__ void store(float* lds, F dst) const {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = (int)threadIdx.x + k * NT;
+      if (e < CNT) lds[dst(e)] = v[k];
+    }
+  }
+};
+
+template <int KIND, int PADW, int NT>
 __device__ __forceinline__ void load_weights(float* lds, const nc_decoder_params& P) {
   using N = Net<KIND, PADW>;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int e = tid; e < N::WEIGHTS; e += nt) lds[e] = 0.f;
-  __syncthreads();
+  constexpr int CDW = N::XYZ ? HID * N::CD : 1, CB = N::XYZ ? HID : 1, NB = N::XYZ ? 3 * EMB : 1;
+  SegRegs<HID * N::in_real(0), NT> w0;
+  SegRegs<HID * N::in_real(1), NT> w1;
+  SegRegs<HID * N::in_real(2), NT> w2;
+  SegRegs<HID * N::in_real(3), NT> w3;
+  SegRegs<HID * N::in_real(4), NT> w4;
+  SegRegs<5 * HID, NT> bl;  // the five biases, gathered below
+  SegRegs<CDW, NT> c0, c1, c2, c3, c4;
+  SegRegs<5 * CB, NT> bc;
+  SegRegs<NB, NT> fb;
+  SegRegs<N::NOUT * HID + N::NOUT, NT> ow;
+  w0.load(P.lin_w[0]); w1.load(P.lin_w[1]); w2.load(P.lin_w[2]); w3.load(P.lin_w[3]); w4.load(P.lin_w[4]);
 #pragma unroll
-  for (int L = 0; L < 5; ++L) {
-    const int in = N::in_real(L), ld = N::lin_ld(L);
-    float* dst = lds + N::lin_off(L);
-    const float* W = P.lin_w[L];
-    for (int e = tid; e < HID * in; e += nt) {
-      const int o = e / in, c = e - o * in;
-      dst[o * ld + N::pack_col(L, c)] = W[e];
-    }
-    for (int e = tid; e < HID; e += nt) lds[N::BL + L * HID + e] = P.lin_b[L][e];
+  for (int k = 0; k < bl.PER; ++k) {  // 5 x 32 biases: tensor e / 32, entry e % 32
+    const int e = (int)threadIdx.x + k * NT;
+    const int L = e >> 5;
+    const float* b = L == 0 ? P.lin_b[0] : L == 1 ? P.lin_b[1] : L == 2 ? P.lin_b[2] : L == 3 ? P.lin_b[3] : P.lin_b[4];
+    bl.v[k] = (e < 5 * HID) ? b[e & 31] : 0.f;
   }
   if constexpr (N::XYZ) {
+    c0.load(P.fc_w[0]); c1.load(P.fc_w[1]); c2.load(P.fc_w[2]); c3.load(P.fc_w[3]); c4.load(P.fc_w[4]);
 #pragma unroll
-    for (int L = 0; L < 5; ++L) {
-      const float* W = P.fc_w[L];
-      float* dst = lds + N::WC + L * HID * N::LDC;
-      for (int e = tid; e < HID * N::CD; e += nt) {
-        const int o = e / N::CD, c = e - o * N::CD;
-        dst[o * N::LDC + c] = W[e];
-      }
-      for (int e = tid; e < HID; e += nt) lds[N::BC + L * HID + e] = P.fc_b[L][e];
+    for (int k = 0; k < bc.PER; ++k) {
+      const int e = (int)threadIdx.x + k * NT;
+      const int L = e >> 5;
+      const float* b = L == 0 ? P.fc_b[0] : L == 1 ? P.fc_b[1] : L == 2 ? P.fc_b[2] : L == 3 ? P.fc_b[3] : P.fc_b[4];
+      bc.v[k] = (e < 5 * HID) ? b[e & 31] : 0.f;
     }
-    for (int e = tid; e < 3 * EMB; e += nt) {
-      const int k = e / EMB, m = e - k * EMB;
-      lds[N::FB + k * EMBP + m] = P.fourier_B[e];
-    }
+    fb.load(P.fourier_B);
   }
-  for (int e = tid; e < N::NOUT * HID; e += nt) lds[N::WO + e] = P.out_w[e];
-  for (int e = tid; e < N::NOUT; e += nt) lds[N::BO + e] = P.out_b[e];
+#pragma unroll
+  for (int k = 0; k < ow.PER; ++k) {
+    const int e = (int)threadIdx.x + k * NT;
+    ow.v[k] = (e < N::NOUT * HID) ? P.out_w[e] : (e < N::NOUT * HID + N::NOUT ? P.out_b[e - N::NOUT * HID] : 0.f);
+  }
+  // zero the image (padding columns / rows stay 0) while the loads are in flight
+  for (int e = threadIdx.x; e < N::WEIGHTS; e += NT) lds[e] = 0.f;
+  __syncthreads();
+  auto lin = [&](int L) {
+    return [=](int e) {
+      const int in = N::in_real(L);
+      const int o = e / in, c = e - o * in;
+      return N::lin_off(L) + o * N::lin_ld(L) + N::pack_col(L, c);
+    };
+  };
+  w0.store(lds, lin(0)); w1.store(lds, lin(1)); w2.store(lds, lin(2)); w3.store(lds, lin(3)); w4.store(lds, lin(4));
+  bl.store(lds, [](int e) { return N::BL + e; });
+  if constexpr (N::XYZ) {
+    auto fc = [&](int L) {
+      return [=](int e) {
+        const int o = e / N::CD, c = e - o * N::CD;
+        return N::WC + L * HID * N::LDC + o * N::LDC + c;
+      };
+    };
+    c0.store(lds, fc(0)); c1.store(lds, fc(1)); c2.store(lds, fc(2)); c3.store(lds, fc(3)); c4.store(lds, fc(4));
+    bc.store(lds, [](int e) { return N::BC + e; });
+    fb.store(lds, [](int e) {
+      const int k = e / EMB, m = e - k * EMB;
+      return N::FB + k * EMBP + m;
+    });
+  }
+  ow.store(lds, [](int e) { return e < N::NOUT * HID ? N::WO + e : N::BO + (e - N::NOUT * HID); });
   __syncthreads();
 }
 
@@ -351,10 +406,10 @@ __device__ __forceinline__ Job pick_job(const Job (&jobs)[MAX_JOBS], unsigned y)
 }
 
 template <int KIND>
-__device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float* lds) {
+__device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float* lds, int64_t wg, int64_t nwg) {
   constexpr int T = FWD_TILES;
   constexpr int CQ = Net<KIND>::CD / 16;
-  load_weights<KIND, PADW_FWD>(lds, ctx.dec[KIND]);
+  load_weights<KIND, PADW_FWD, FWD_THREADS>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
   const int64_t per = 16 * waves * T;  // points per workgroup iteration
@@ -377,8 +432,8 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
         nc[t][q] = ok ? *reinterpret_cast<const float4*>(cf + 16 * q) : float4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  load_inputs(blockIdx.x);
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+  load_inputs(wg);
+  for (int64_t blk = wg; blk < nblk; blk += nwg) {
     // keep the (loop-invariant) LDS weight reads inside the loop: hoisting all of
     // them out of the persistent loop would need thousands of registers
     asm volatile("" ::: "memory");
@@ -400,7 +455,7 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
       rec[t] = (ctx.save_rec && pt[t] < ctx.P) ? ctx.rec + job.rec_off + pt[t] * Rec<KIND>::STRIDE : nullptr;
 #endif
     }
-    load_inputs(blk + gridDim.x);
+    load_inputs(blk + nwg);
     float out[T][4];
     wave_forward<KIND, T>(lds, i, g, R, out, rec);
 #pragma unroll
@@ -419,14 +474,23 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
   }
 }
 
+// job of workgroup b in a 1-D grid split [off[0], off[1]), [off[1], off[2]), ...
+__device__ __forceinline__ int job_of_wg(const int32_t (&off)[MAX_JOBS + 1], int b) {
+  return (b >= off[1] ? 1 : 0) + (b >= off[2] ? 1 : 0);
+}
+
 __global__ void __launch_bounds__(FWD_THREADS) k_mlp_fwd(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Job job = pick_job(ctx.jobs, blockIdx.y);
+  const int b = blockIdx.x;
+  const int j = job_of_wg(ctx.fwd_off, b);
+  const Job job = pick_job(ctx.jobs, j);
+  const int o0 = j == 0 ? ctx.fwd_off[0] : (j == 1 ? ctx.fwd_off[1] : ctx.fwd_off[2]);
+  const int o1 = j == 0 ? ctx.fwd_off[1] : (j == 1 ? ctx.fwd_off[2] : ctx.fwd_off[3]);
   switch (job.kind) {
-    case K_COARSE: fwd_job<K_COARSE>(ctx, job, lds); break;
-    case K_MID: fwd_job<K_MID>(ctx, job, lds); break;
-    case K_FINE: fwd_job<K_FINE>(ctx, job, lds); break;
-    default: fwd_job<K_COLOR>(ctx, job, lds); break;
+    case K_COARSE: fwd_job<K_COARSE>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_MID: fwd_job<K_MID>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_FINE: fwd_job<K_FINE>(ctx, job, lds, b - o0, o1 - o0); break;
+    default: fwd_job<K_COLOR>(ctx, job, lds, b - o0, o1 - o0); break;
   }
 }
 
@@ -475,7 +539,7 @@ template <int KIND>
 __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float* lds) {
   using N = Net<KIND>;
   using RC = Rec<KIND>;
-  load_weights<KIND, PADW_BWD>(lds, ctx.dec[KIND]);
+  load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int waves = blockDim.x >> 6;
@@ -721,7 +785,7 @@ struct DwTiles {
 constexpr int DW_WAVES = DW_THREADS / 64;
 
 template <int KIND>
-__device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float* lds) {
+__device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float* lds, int64_t wg, int64_t nwg) {
   using N = Net<KIND>;
   using RC = Rec<KIND>;
   using LY = DwLayout<KIND>;
@@ -808,8 +872,8 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
       pre[k] = (e < ITEMS && e < lim) ? blk[e] : float4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  if (blockIdx.x < nsub) prefetch(blockIdx.x);
-  for (int64_t sub = blockIdx.x; sub < nsub; sub += gridDim.x) {
+  if (wg < nsub) prefetch(wg);
+  for (int64_t sub = wg; sub < nsub; sub += nwg) {
     __syncthreads();  // previous sub-chunk's reads are done
     const int64_t p0 = sub * DW_NPTS;
 #ifndef NC_ABL_DW_NO_STAGE  // timing-only ablation: records not copied into LDS
@@ -844,7 +908,7 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
 #endif
     __syncthreads();
 #ifndef NC_ABL_DW_NO_LOAD  // timing-only ablation: the next records are not loaded
-    if (sub + gridDim.x < nsub) prefetch(sub + gridDim.x);
+    if (sub + nwg < nsub) prefetch(sub + nwg);
 #endif
     // ---- tiles: DW_NPTS/4 k-steps of 4 points; the wave's NS accumulation chains are
     // interleaved (k-step outer) so no MFMA waits on its predecessor's result ----
@@ -879,7 +943,7 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
   }
   // ---- flush: every weight-gradient element is owned by exactly one lane and
   // every bias by one bacc entry, so the slab row is written without an image ----
-  float* slab = ctx.slab + ((int64_t)blockIdx.y * ctx.slab_wgs + blockIdx.x) * ctx.slab_stride;
+  float* slab = ctx.slab + (int64_t)blockIdx.x * ctx.slab_stride;  // one row per workgroup
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int tau = wv + DW_WAVES * s;
@@ -904,13 +968,17 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
 
 __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Job job = pick_job(ctx.jobs, blockIdx.y);
+  const int b = blockIdx.x;
+  const int j = job_of_wg(ctx.dw_off, b);
+  const Job job = pick_job(ctx.jobs, j);
   if (!job.need_dw) return;
+  const int o0 = j == 0 ? ctx.dw_off[0] : (j == 1 ? ctx.dw_off[1] : ctx.dw_off[2]);
+  const int o1 = j == 0 ? ctx.dw_off[1] : (j == 1 ? ctx.dw_off[2] : ctx.dw_off[3]);
   switch (job.kind) {
-    case K_COARSE: dw_job<K_COARSE>(ctx, job, lds); break;
-    case K_MID: dw_job<K_MID>(ctx, job, lds); break;
-    case K_FINE: dw_job<K_FINE>(ctx, job, lds); break;
-    default: dw_job<K_COLOR>(ctx, job, lds); break;
+    case K_COARSE: dw_job<K_COARSE>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_MID: dw_job<K_MID>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_FINE: dw_job<K_FINE>(ctx, job, lds, b - o0, o1 - o0); break;
+    default: dw_job<K_COLOR>(ctx, job, lds, b - o0, o1 - o0); break;
   }
 }
 
@@ -980,10 +1048,19 @@ int mlp_blocks_per_cu(int which) {
   return cache[dev][which];
 }
 
-int launch_mlp_fwd(const MlpCtx& c, int grid_x, hipStream_t s) {
+int decoder_macs(int kind) {  // SURVEY.md §8a a10-a11 (MAC per point)
+  switch (kind) {
+    case K_COARSE: return 6176;
+    case K_MID: return 15479;
+    case K_FINE: return 20599;
+    default: return 15575;
+  }
+}
+
+int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
   static int attr = -1;
   if (attr != 0 && (attr = set_lds(k_mlp_fwd, mlp_fwd_lds_bytes())) != 0) return attr;
-  hipLaunchKernelGGL(k_mlp_fwd, dim3(grid_x, c.n_jobs), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
+  hipLaunchKernelGGL(k_mlp_fwd, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 
@@ -999,7 +1076,7 @@ int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s) {
 int launch_mlp_dw(const MlpCtx& c, hipStream_t s) {
   static int attr = -1;
   if (attr != 0 && (attr = set_lds(k_mlp_dw, mlp_dw_lds_bytes())) != 0) return attr;
-  hipLaunchKernelGGL(k_mlp_dw, dim3(c.slab_wgs, c.n_jobs), dim3(DW_THREADS), mlp_dw_lds_bytes(), s, c);
+  hipLaunchKernelGGL(k_mlp_dw, dim3(c.dw_off[c.n_jobs]), dim3(DW_THREADS), mlp_dw_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 

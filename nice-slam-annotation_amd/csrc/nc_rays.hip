@@ -458,8 +458,10 @@ __global__ void __launch_bounds__(PR_COLS * PR_PARTS) k_param_reduce(const Param
   if ((int64_t)blockIdx.x * PR_COLS * 4 >= np) return;          // whole workgroup past the end
   float4 acc = float4{0.f, 0.f, 0.f, 0.f};
   if (e < c.slab_stride) {  // slab rows are padded to slab_stride (multiple of 64 floats)
-    const float* src = c.slab + (int64_t)j * c.slab_wgs * c.slab_stride + e;
-    for (int w = prt; w < c.slab_wgs; w += PR_PARTS) {
+    const int w0 = j == 0 ? c.wg_off[0] : (j == 1 ? c.wg_off[1] : c.wg_off[2]);
+    const int w1 = j == 0 ? c.wg_off[1] : (j == 1 ? c.wg_off[2] : c.wg_off[3]);
+    const float* src = c.slab + (int64_t)w0 * c.slab_stride + e;
+    for (int w = prt; w < w1 - w0; w += PR_PARTS) {
       const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)w * c.slab_stride);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
