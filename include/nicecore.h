@@ -139,6 +139,12 @@ typedef struct nc_render_args {
   const float* loss_color;  /* [N,3] target colour; required with NC_LOSS_COLOR */
   double* loss_out;         /* device scalar */
   const double* g_loss;     /* device scalar upstream gradient of the loss (NULL = 0) */
+  /* optional (ABI v4): the forward zero-fills grad_zero[0 .. grad_zero_floats) beside its
+   * grid gathers -- e.g. the gradient buffer the backward will accumulate the grids'
+   * gradients into -- instead of the caller launching a fill (16-B aligned, multiple
+   * of 4 floats). */
+  float* grad_zero;
+  int64_t grad_zero_floats;
 } nc_render_args;
 
 typedef struct nc_points_args {

@@ -84,6 +84,10 @@ int cu_count() {
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// up to this many rays every k_ray_setup workgroup reduces max(gt_depth) itself
+// (<= 16 KB of L2 reads per workgroup) instead of a separate k_depth_max launch
+constexpr int64_t kDmaxLocalRays = 4096;
+
 struct Plan {
   int n_jobs = 0;
   Job jobs[MAX_JOBS];
@@ -528,14 +532,27 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   }
   if (!a->rays_o || !a->rays_d || !a->depth || !a->var || !a->color)
     return fail(-1, "nicecore: NULL ray input or output pointer");
-  if (a->gt_depth && !a->depth_max)
-    if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) return e;
   RayCtx rc;
   fill_ray(rc, a, pl, ws, w, P, S);
+  if (a->gt_depth && !a->depth_max) {
+    if (a->n_rays <= kDmaxLocalRays) {
+      rc.dmax_local = 1;  // reduced inside k_ray_setup
+    } else if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) {
+      return e;
+    }
+  }
   if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
+  if (a->grad_zero && a->grad_zero_floats > 0) {  // the caller's gradient buffer, zeroed by the gather
+    if ((reinterpret_cast<uintptr_t>(a->grad_zero) & 15) || (a->grad_zero_floats & 3))
+      return fail(-1, "nicecore: grad_zero must be 16-byte aligned and a multiple of 4 floats");
+    m.zero_fill = reinterpret_cast<float4*>(a->grad_zero);
+    m.zero_n4 = a->grad_zero_floats / 4;
+  }
   if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
+  m.zero_fill = nullptr;
+  m.zero_n4 = 0;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
   if (int e = check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd")) return e;
   if (a->loss != NC_LOSS_NONE)

@@ -24,6 +24,15 @@ __global__ void __launch_bounds__(256) k_grid_gather(const MlpCtx ctx) {
   const int lg = (job.kind == K_FINE && !ctx.share_mid) ? 4 : 3;  // log2(chunks per point)
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = t >> lg;
+  if (ctx.zero_fill) {  // the backward's gradient buffer, zeroed beside the gathers (stores last:
+                        // nothing waits on them in this thread)
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x * gridDim.y;
+    const int64_t tid = (int64_t)blockIdx.y * gridDim.x * blockDim.x + t;
+    if (p >= ctx.P) {
+      for (int64_t z = tid; z < ctx.zero_n4; z += nthr) ctx.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
+  }
   if (p >= ctx.P) return;
   const int q = (int)(t & ((1 << lg) - 1));
   const int gk = q < 8 ? job.kind : K_MID;
@@ -61,6 +70,11 @@ __global__ void __launch_bounds__(256) k_grid_gather(const MlpCtx ctx) {
   *reinterpret_cast<float4*>(ctx.cfeat + job.c_off + p * job.c_stride + 4 * q) = o;
   if (ctx.share_mid && y == 1)  // the fine decoder's no-grad grid_middle lookup is this one
     *reinterpret_cast<float4*>(ctx.cfeat + ctx.jobs[0].c_off + p * ctx.jobs[0].c_stride + 32 + 4 * q) = o;
+  if (ctx.zero_fill) {
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x * gridDim.y;
+    const int64_t tid = (int64_t)blockIdx.y * gridDim.x * blockDim.x + t;
+    for (int64_t z = tid; z < ctx.zero_n4; z += nthr) ctx.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
+  }
 }
 
 int launch_grid_gather(const MlpCtx& c, hipStream_t s) {

@@ -51,6 +51,8 @@ struct MlpCtx {
   int32_t fwd_off[MAX_JOBS + 1];  // k_mlp_fwd: workgroups [off[j], off[j+1]) of the 1-D grid run job j
   int32_t dw_off[MAX_JOBS + 1];   // k_mlp_dw: same, and slab row = workgroup index
                                   // (both split in proportion to the decoders' per-point MACs)
+  float4* zero_fill;         // optional: k_grid_gather also zero-fills zero_n4 float4s here (the
+  int64_t zero_n4;           // caller's gradient buffer, nc_render_args.grad_zero)
   float* dfeat;              // NC_DETERMINISTIC: [n_jobs][P][32] d features of each job's own grid
                              // (k_mlp_dx stores them instead of scattering with atomics), else NULL
 };
@@ -91,6 +93,8 @@ struct RayCtx {
   const float* rays_d;
   const float* gt_depth;
   const float* depth_max;  // device scalar (user override or computed into the workspace)
+  int32_t dmax_local;      // k_ray_setup reduces max(gt_depth) itself, per workgroup (small N):
+                           // no k_depth_max launch
   double bound[3][2];
   float t_strat[NC_MAX_SAMPLES];
   double t_surf[NC_MAX_SURF];

@@ -53,6 +53,24 @@ __device__ __forceinline__ double min_nan(double a, double b) { return (a < b ||
 __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  float dmax_blk = 0.f;
+  if (c.dmax_local) {  // torch.max(gt_depth) over the whole batch, by every workgroup (N small)
+    __shared__ float red[RAY_WAVES];
+    float m = -INFINITY;
+    for (int64_t k = threadIdx.x; k < c.N; k += blockDim.x) {
+      const float v = c.gt_depth[k];
+      m = (v > m || isnan(v)) ? v : m;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v = __shfl_xor(m, o);
+      m = (v > m || isnan(v)) ? v : m;
+    }
+    if (lane == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = red[0];
+    for (int w = 1; w < RAY_WAVES; ++w) m = (red[w] > m || isnan(red[w])) ? red[w] : m;
+    dmax_blk = m;
+  }
   if (r >= c.N) return;
   double o[3], d[3];
 #pragma unroll
@@ -75,7 +93,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   float gd = 0.f, dmax = 0.f;
   if (has_depth) {
     gd = c.gt_depth[r];
-    dmax = *c.depth_max;
+    dmax = c.dmax_local ? dmax_blk : *c.depth_max;
     const double hi = (double)(dmax * 1.2f);  // torch.max(gt_depth*1.2) (float32)
     double v = far_bb < 0.0 ? 0.0 : far_bb;   // torch.clamp(far_bb, 0, hi)
     far = v > hi ? hi : v;

@@ -53,7 +53,8 @@ class NcRenderArgs(ctypes.Structure):
                 ("g_depth", c_void_p), ("g_var", c_void_p), ("g_color", c_void_p),
                 ("g_rays_o", c_void_p), ("g_rays_d", c_void_p),
                 ("loss", c_int32), ("loss_flags", c_int32), ("w_color", c_double),
-                ("loss_depth", c_void_p), ("loss_color", c_void_p), ("loss_out", c_void_p), ("g_loss", c_void_p)]
+                ("loss_depth", c_void_p), ("loss_color", c_void_p), ("loss_out", c_void_p), ("g_loss", c_void_p),
+                ("grad_zero", c_void_p), ("grad_zero_floats", c_int64)]
 
 
 class NcPointsArgs(ctypes.Structure):

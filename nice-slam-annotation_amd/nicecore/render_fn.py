@@ -59,6 +59,11 @@ def deterministic_requested(spec=None) -> bool:
     return os.environ.get("NC_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
 
 
+# the forward zero-fills the backward's grid-gradient buffer (nc_render_args.grad_zero);
+# NICECORE_FWD_ZERO=0 falls back to a separate fill in the backward (A/B timing)
+_FWD_ZERO = os.environ.get("NICECORE_FWD_ZERO", "1") != "0"
+
+
 def _flags(ctx, spec):
     if not any(ctx.needs_input_grad):
         return 0
@@ -258,7 +263,16 @@ class _Plan:
 _PLANS = weakref.WeakKeyDictionary()  # decoders module -> {stage: _Plan}
 
 
-def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device):
+def _grad_sizes(lib, plan, needs_params, needs_grids, grids):
+    sl = plan.param_slices()
+    gk = [k for k in plan.grids if needs_grids[k]]
+    pk = [k for k in plan.decs if any(needs_params[sl[k][0]:sl[k][1]])]
+    gsize = sum(grids[k].numel() for k in gk)
+    psize = {k: int(lib.nc_param_count(k)) for k in pk}
+    return gk, pk, gsize, psize
+
+
+def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device, prezeroed=None):
     """Every gradient of one backward call lives in ONE float32 buffer: the grid
     gradients first (strided views with each grid's own memory format, zero-filled
     by a single kernel), then one flat parameter vector per decoder whose
@@ -266,14 +280,13 @@ def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device):
     views are stolen by AccumulateGrad as the leaves' .grad (their strides obey
     the layout contract), and distributed.allreduce_grads reduces the shared
     buffer with one collective."""
-    sl = plan.param_slices()
-    gk = [k for k in plan.grids if needs_grids[k]]
-    pk = [k for k in plan.decs if any(needs_params[sl[k][0]:sl[k][1]])]
-    gsize = sum(grids[k].numel() for k in gk)
-    psize = {k: int(lib.nc_param_count(k)) for k in pk}
-    buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
-    if gsize:
-        buf[:gsize].zero_()
+    gk, pk, gsize, psize = _grad_sizes(lib, plan, needs_params, needs_grids, grids)
+    if prezeroed is not None and prezeroed.numel() == gsize + sum(psize.values()):
+        buf = prezeroed  # grid part zero-filled by the forward (nc_render_args.grad_zero)
+    else:
+        buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
+        if gsize:
+            buf[:gsize].zero_()
     grid_grads = [None] * 4
     off = 0
     for k in plan.grids:
@@ -369,12 +382,22 @@ class NiceRenderFn(torch.autograd.Function):
             loss = torch.empty((), device=device, dtype=torch.float64)
             a.loss, a.loss_flags, a.w_color = kind, lflags, float(w)
             a.loss_depth, a.loss_color, a.loss_out = tgt[0].data_ptr(), _ptr(tgt[1]), loss.data_ptr()
+        # the backward's gradient buffer: allocated here and zero-filled by the forward's
+        # gather kernel (no separate fill launch); used by the first backward call
+        ctx.grad_buf = None
+        if _FWD_ZERO and any(ctx.needs_input_grad[4:8]):
+            _, _, gsize, psize = _grad_sizes(lib, plan, ctx.needs_input_grad[8:], ctx.needs_input_grad[4:8],
+                                             (g0, g1, g2, g3))
+            if gsize:
+                ctx.grad_buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
+                a.grad_zero, a.grad_zero_floats = ctx.grad_buf.data_ptr(), gsize
         nbytes = lib.nc_render_workspace_bytes(ctypes.byref(a))
         if nbytes == 0:
             L.check(-1, "nc_render_workspace_bytes")
         ws = torch.empty(nbytes, device=device, dtype=torch.uint8)
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_render_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_render_forward")
+        a.grad_zero, a.grad_zero_floats = None, 0
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
         ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt)
         ctx.grids = grids
@@ -403,7 +426,9 @@ class NiceRenderFn(torch.autograd.Function):
             g_rd = g_rd if g_rd is not None else torch.empty_like(rays_o)
         a.g_rays_o, a.g_rays_d = _ptr(g_ro), _ptr(g_rd)
         needs_params = need[8:]
-        grid_grads, flats = _alloc_grads(lib, plan, needs_params, need[4:8], ctx.grids, a, device)
+        grid_grads, flats = _alloc_grads(lib, plan, needs_params, need[4:8], ctx.grids, a, device,
+                                         prezeroed=ctx.grad_buf)
+        ctx.grad_buf = None  # a second backward (retain_graph) gets a fresh, zeroed buffer
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_render_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
                 "nc_render_backward")
