@@ -84,9 +84,13 @@ def build_workload(args, rank, device):
     from nicecore import scene as S
     from nicecore.renderer import Renderer
     sc = S.make_scene(args.scene)
-    gen = torch.Generator().manual_seed(0)
-    grids = S.init_grids(sc.shapes, generator=gen, device=device,
-                         channels_last=(args.layout == "channels_last"))
+    if S.grids_bytes(sc.shapes) > (2 << 30):  # C5-sized grids: generated in HBM, no host copy
+        grids = S.init_grids_device(sc.shapes, seed=rank, device=device,
+                                    channels_last=(args.layout == "channels_last"))
+    else:
+        gen = torch.Generator().manual_seed(0)
+        grids = S.init_grids(sc.shapes, generator=gen, device=device,
+                             channels_last=(args.layout == "channels_last"))
     model = D.build_default_nice(seed=0).to(device)
     model.bound = sc.bound.to(device)
     for n in ("middle", "fine", "color"):
@@ -362,7 +366,12 @@ def main():
         "kernels_ms": {k: round(v, 4) for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1])},
     }
     if world == 1 and rank == 0 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        from nicecore import scene as S_
+        if S_.grids_bytes(S_.make_scene(args.scene).shapes) > (8 << 30):
+            out["cpu_baseline"] = {"value": None, "unit": "rays/s", "cores": None, "kind": "port",
+                                   "sample": "not run: the scene's grids do not fit a bounded CPU sample"}
+        else:
+            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

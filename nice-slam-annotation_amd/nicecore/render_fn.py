@@ -263,6 +263,16 @@ class _Plan:
 _PLANS = weakref.WeakKeyDictionary()  # decoders module -> {stage: _Plan}
 
 
+def _dense_strides(g):
+    """The grid's own strides when it is dense (contiguous or channels_last_3d, the
+    layouts AccumulateGrad keeps), else contiguous strides: a strided view of a larger
+    tensor gets a dense gradient of its own shape."""
+    if g.is_contiguous(memory_format=torch.channels_last_3d) or g.is_contiguous():
+        return g.stride()
+    C, D, H, W = g.shape[1:]
+    return (C * D * H * W, D * H * W, H * W, W, 1)
+
+
 def _grad_sizes(lib, plan, needs_params, needs_grids, grids):
     sl = plan.param_slices()
     gk = [k for k in plan.grids if needs_grids[k]]
@@ -293,7 +303,7 @@ def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device, prez
         args.grids[k].grad = None
     for k in gk:
         g = grids[k]
-        gg = torch.as_strided(buf, g.shape, g.stride(), off)
+        gg = torch.as_strided(buf, g.shape, _dense_strides(g), off)
         args.grids[k].grad = gg.data_ptr()
         st = gg.stride()
         for ax in range(4):

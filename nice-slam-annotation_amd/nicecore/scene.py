@@ -40,6 +40,13 @@ PRESETS = {
         bound=[[-5.8, 11.3], [-4.0, 4.5], [-7.9, 4.9]],
         H=720, W=1280, fx=607.4694213867188, fy=607.4534912109375,
         cx=636.9967041015625, cy=369.2689514160156, crop_edge=0),
+    # BASELINE.json configs[4] (C5): synthetic 10 m x 10 m x 3 m scene whose fine and
+    # colour grids (0.0118 m) hold ~204M voxels = 26.1 GB each (SURVEY.md §8 header);
+    # Replica intrinsics for the synthetic rays.
+    "synthetic_c5": dict(
+        bound=[[0.0, 10.0], [0.0, 10.0], [0.0, 3.0]],
+        H=680, W=1200, fx=600.0, fy=600.0, cx=599.5, cy=339.5, crop_edge=0,
+        grid_len=dict(coarse=2.0, middle=0.0236, fine=0.0118, color=0.0118, bound_divisible=0.32)),
     # Tiny scene used by the golden fixtures (grids of a few tens of KB).
     "tiny": dict(
         bound=[[-1.0, 1.0], [-0.5, 0.5], [-0.5, 0.5]],
@@ -107,6 +114,25 @@ def init_grids(shapes: dict, c_dim: int = C_DIM, generator=None, device="cpu",
     return grids
 
 
+def init_grids_device(shapes: dict, seed: int, device, c_dim: int = C_DIM, channels_last: bool = True,
+                      std: dict | None = None) -> dict:
+    """N(0, std) grids generated directly in device memory (the multi-GB grids of C5:
+    no host copy).  Seeded by a device generator, so not the CPU init's values."""
+    std = GRID_STD if std is None else std
+    gen = torch.Generator(device=device).manual_seed(seed)
+    fmt = torch.channels_last_3d if channels_last else torch.contiguous_format
+    grids = {}
+    for key in GRID_KEYS:
+        if key in shapes:
+            t = torch.empty([1, c_dim, *shapes[key]], device=device, memory_format=fmt)
+            grids[key] = t.normal_(mean=0, std=std[key], generator=gen)
+    return grids
+
+
+def grids_bytes(shapes: dict, c_dim: int = C_DIM) -> int:
+    return sum(4 * c_dim * int(np.prod(s)) for s in shapes.values())
+
+
 def decoder_bounds(bound: torch.Tensor, coarse_bound_enlarge=COARSE_BOUND_ENLARGE):
     """Per-decoder ``.bound`` as assigned by src/NICE_SLAM.py:202-208."""
     return {"coarse": bound * coarse_bound_enlarge, "middle": bound,
@@ -130,7 +156,7 @@ class SceneSpec:
 
 def make_scene(name: str, grid_len: dict | None = None) -> SceneSpec:
     p = PRESETS[name]
-    gl = dict(DEFAULT_GRID_LEN if grid_len is None else grid_len)
+    gl = dict(grid_len if grid_len is not None else p.get("grid_len", DEFAULT_GRID_LEN))
     bound = snap_bound(p["bound"], gl["bound_divisible"])
     H, W, cx, cy = p["H"], p["W"], p["cx"], p["cy"]
     ce = p.get("crop_edge", 0)
