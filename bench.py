@@ -243,18 +243,21 @@ def cpu_baseline(args, seconds):
                       f"{args.mode} grads, torch CPU fp32/fp64 oracle, {threads} threads"}
 
 
-def read_traffic():
+def read_traffic(args):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc
-    summary (profiles/*traffic*.json), if present."""
+    summary (profiles/*traffic*.json) measured on this same workload, if present."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*traffic*.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            return json.load(f)
-    except Exception:
-        return None
+    want = {"scene": args.scene, "rays": args.rays, "stage": args.stage, "mode": args.mode,
+            "layout": args.layout}
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "*traffic*.json")), reverse=True):
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if d.get("config") == want:
+            return d
+    return None
 
 
 class _NullTimer:
@@ -334,7 +337,7 @@ def main():
     if fl is not None and by and avg_ms > 0:
         tflops = fl / (avg_ms * 1e-3) / 1e12
         gbs = by / (avg_ms * 1e-3) / 1e9
-        tr = read_traffic()
+        tr = read_traffic(args)
         traffic = ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes")
         ridge = FP32_MFMA_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # FLOP per byte
         hbm_bound = fl / by < ridge
