@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse "
                          "the multi-rank path on one GPU)")
+    ap.add_argument("--sparse-grads", default="auto", choices=["auto", "on", "off"],
+                    help="grid gradients as touched-voxel rows (nicecore.sparse); auto = on for "
+                         "grids too large for a dense gradient per iteration (C5)")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -106,9 +109,15 @@ def build_workload(args, rank, device):
         g.requires_grad_(ba)
     for p in model.parameters():
         p.requires_grad_(ba)
+    sparse = None
+    if ba and (args.sparse_grads == "on" or
+               (args.sparse_grads == "auto" and S.grids_bytes(sc.shapes) > (2 << 30))):
+        from nicecore.sparse import SparseGridGrads
+        # rows for every corner of every lookup of one step: no growth after the first step
+        sparse = SparseGridGrads(grids, capacity=8 * args.rays * 48)
     w = dict(sc=sc, grids=grids, model=model, renderer=renderer,
              ro=ro.to(device).requires_grad_(True), rd=rd.to(device).requires_grad_(True),
-             gt=dep.to(device), gtc=col.to(device), ba=ba)
+             gt=dep.to(device), gtc=col.to(device), ba=ba, sparse=sparse)
     return w
 
 
@@ -130,7 +139,8 @@ def make_step(w, args, world, device):
     grids, model, renderer = w["grids"], w["model"], w["renderer"]
     ro, rd, gt, gtc = w["ro"], w["rd"], w["gt"], w["gtc"]
     params = [p for p in model.parameters() if p.requires_grad]
-    gvals = [g for g in grids.values() if g.requires_grad]
+    sparse = w["sparse"]
+    gvals = [g for k, g in grids.items() if g.requires_grad and (sparse is None or k not in sparse.rows)]
     dmax = gt.max().reshape(1).clone() if world > 1 else None  # static buffer
     loss_kw = LOSS_KW[args.mode](args.stage)
 
@@ -142,16 +152,21 @@ def make_step(w, args, world, device):
     def body():
         for t in params + gvals + [ro, rd]:
             t.grad = None
+        if sparse is not None:  # touched-voxel grid gradients: forget last step's rows
+            sparse.zero_grad()
         # render_batch_ray + the caller's loss in the same launches (k_loss):
         # Mapper.py:603-612 (BA mode) / Tracker.py:117-131 (tracker mode)
         depth, unc, color, loss = renderer.render_batch_loss(
-            grids, model, rd, ro, device, args.stage, gt, gtc, **loss_kw, depth_max=dmax)
+            grids, model, rd, ro, device, args.stage, gt, gtc, **loss_kw, depth_max=dmax,
+            sparse_grads=sparse)
         loss.backward()
         return loss
 
     def post():
         if world > 1 and w["ba"]:  # one RCCL SUM over the core's shared gradient buffer
             ND.allreduce_grads(gvals + params)
+            if sparse is not None:  # union of the ranks' touched voxels, then one SUM per grid
+                sparse.allreduce()
 
     def eager():
         pre()
@@ -362,7 +377,8 @@ def main():
         "config": {"workload": f"{args.scene} {args.rays} rays x {S} samples per GPU, stage {args.stage}, "
                                f"{'mapper/BA grads (rays+grids+decoders)' if args.mode == 'ba' else 'tracker grads (rays)'}",
                    "rays_per_gpu": args.rays, "samples_per_ray": S, "stage": args.stage,
-                   "mode": args.mode, "grid_layout": args.layout, "parallelism": f"dp{world}"},
+                   "mode": args.mode, "grid_layout": args.layout, "parallelism": f"dp{world}",
+                   "grid_grads": "sparse rows" if w["sparse"] is not None else "dense"},
         "roofline": roof,
         "launch": "hipGraph replay" if graphed is not None else "eager",
         "eager_ms_per_step": round(eager_ms, 4),

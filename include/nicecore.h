@@ -20,6 +20,11 @@
  *                       pose gradient (Tracker.py:95-111, Mapper.py:543-591).
  *   nc_frustum_mask     src/Mapper.py:100-187 get_mask_from_c2w (frustum feature
  *                       selection of one grid).
+ *   nc_sparse_rows_*    the touched-voxel gradient of a feature grid too large for a
+ *                       dense gradient: the reference's dense
+ *                       grid.grad / val[mask] gradient (Mapper.py:392-404, :620-627)
+ *                       restricted to the voxels the batch touched, and its
+ *                       multi-rank union before the RCCL sum.
  *
  * Conventions
  *   - All pointers are device pointers on the current HIP device; the library
@@ -47,7 +52,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 4
+#define NC_ABI_VERSION 5
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -74,13 +79,30 @@ enum nc_decoder { NC_DEC_COARSE = 0, NC_DEC_MIDDLE = 1, NC_DEC_FINE = 2, NC_DEC_
 
 /* One feature grid c['grid_*'], shape [1, 32, D, H, W] float32 (NICE_SLAM.py:243-320).
  * Strides are in elements for the C, D, H, W axes; channel stride 1
- * (torch.channels_last_3d) is the fast path. */
+ * (torch.channels_last_3d) is the fast path.
+ *
+ * Sparse gradient rows (ABI v5, optional; grad_rows != NULL): instead of a dense
+ * [1,32,D,H,W] gradient, `grad` is a compact [row_capacity][32] float buffer (row
+ * stride 32, channel stride 1; grad_stride is ignored) holding one row per touched
+ * voxel.  grad_rows is a [D*H*W] int32 map voxel (z*H + y)*W + x -> row, -1 where
+ * the voxel has no row (all -1 the first time; nc_sparse_rows_clear restores that).
+ * A forward with NC_SAVE_FOR_BACKWARD claims a row for every in-bounds corner of
+ * every lookup that will receive a grid gradient (first come, first served: the row
+ * order is not deterministic), zero-fills it and records its voxel in row_voxel;
+ * *row_count counts the rows.  Claims accumulate over forwards until cleared, so
+ * several forwards may precede one backward.  row_capacity >= 8 x the lookups of
+ * the batch (or D*H*W) never overflows; an overflowing claim is dropped and flagged
+ * by *row_count > row_capacity.  The backward accumulates into the rows. */
 typedef struct nc_grid {
   const float* data;
   float* grad;            /* NULL: no gradient wanted for this grid */
   int64_t dims[3];        /* D, H, W */
   int64_t stride[4];      /* C, D, H, W strides of data */
   int64_t grad_stride[4]; /* C, D, H, W strides of grad */
+  int32_t* grad_rows;     /* sparse mode: [D*H*W] voxel -> gradient row, or NULL (dense) */
+  int64_t* row_voxel;     /* [row_capacity] voxel of each row */
+  int32_t* row_count;     /* device counter of claimed rows */
+  int64_t row_capacity;
 } nc_grid;
 
 /* Parameters of one decoder, pointers to the nn.Parameter storage (contiguous,
@@ -240,6 +262,33 @@ typedef struct nc_frustum_args {
 
 int nc_frustum_mask(const nc_frustum_args* args, void* stream);
 
+/* Sparse gradient rows of one grid (ABI v5; see nc_grid). */
+typedef struct nc_sparse_rows {
+  int32_t* grad_rows;   /* [n_voxels] voxel -> row map */
+  int64_t n_voxels;     /* D*H*W */
+  int64_t* row_voxel;   /* [capacity] */
+  int32_t* row_count;   /* device scalar */
+  int64_t capacity;
+  float* values;        /* [capacity][32] gradient rows */
+} nc_sparse_rows;
+
+/* Reset the map entries of the claimed rows to -1 and *row_count to 0 (the sparse
+ * counterpart of zeroing grid.grad; the rows' values are zeroed when re-claimed). */
+int nc_sparse_rows_clear(const nc_sparse_rows* rows, void* stream);
+
+/* Multi-rank union of the touched-voxel sets before the gradient sum (RCCL):
+ * all_voxel[r * rank_capacity + i] for i < all_count[r] are rank r's rows (the
+ * all-gathered row_voxel / row_count of every rank, this one included).  Writes
+ * `out`: the union, ascending by voxel -- identical on every rank -- as out->row_voxel
+ * / *out->row_count, out->values = this rank's gradient rows permuted into that
+ * order (zero where this rank has none), and the shared map in->grad_rows ==
+ * out->grad_rows re-pointed to the new rows.  out->capacity >= the union's size
+ * (world * rank_capacity always suffices).  Scratch: nc_sparse_merge_temp_bytes. */
+size_t nc_sparse_merge_temp_bytes(int64_t n_keys, int64_t n_voxels);
+int nc_sparse_rows_merge(const nc_sparse_rows* in, const nc_sparse_rows* out, const int64_t* all_voxel,
+                         const int32_t* all_count, int32_t world, int64_t rank_capacity, void* temp,
+                         size_t temp_bytes, void* stream);
+
 int nc_abi_version(void);
 const char* nc_last_error(void);
 
@@ -247,7 +296,8 @@ const char* nc_last_error(void);
 int64_t nc_param_count(int decoder);
 
 /* sizeof() of the ABI structs, for binding-layout checks:
- * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params, 4 nc_sample_args, 5 nc_frustum_args. */
+ * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params, 4 nc_sample_args, 5 nc_frustum_args,
+ * 6 nc_sparse_rows. */
 size_t nc_struct_size(int which);
 
 size_t nc_render_workspace_bytes(const nc_render_args* args);

@@ -36,13 +36,14 @@ int check_hip(int e, const char* what) {
 enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
-  KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_COUNT
+  KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
+  KID_ROWS_MERGE, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
-                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask"};
+                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -119,6 +120,14 @@ int check_grid(const nc_grid& g, const char* name) {
   if (!g.data) return fail(-1, std::string("nicecore: grid ") + name + " is required by this stage but NULL");
   for (int k = 0; k < 3; ++k)
     if (g.dims[k] < 1) return fail(-1, std::string("nicecore: grid ") + name + " has an empty dimension");
+  if (g.grad_rows) {  // sparse gradient rows (ABI v5)
+    if (!g.row_voxel || !g.row_count || g.row_capacity < 1 || !g.grad ||
+        (reinterpret_cast<uintptr_t>(g.grad) & 15))
+      return fail(-1, std::string("nicecore: grid ") + name +
+                          " has grad_rows but no 16-B aligned gradient rows, row_voxel, row_count or capacity");
+    if (g.row_capacity > INT32_MAX || g.dims[0] * g.dims[1] * g.dims[2] > INT32_MAX)
+      return fail(-1, std::string("nicecore: grid ") + name + ": sparse rows need < 2^31 voxels and rows");
+  }
   return 0;
 }
 
@@ -288,6 +297,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.slab = at<float>(ws, w.slab);
   m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
   m.cfeat = w.save ? m.rec : at<float>(ws, w.feat);
+  m.claim_rows = w.save;  // only grids with a row map (nc_grid.grad_rows) claim
   m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
 }
 
@@ -504,6 +514,7 @@ size_t nc_struct_size(int which) {
     case 3: return sizeof(nc_decoder_params);
     case 4: return sizeof(nc_sample_args);
     case 5: return sizeof(nc_frustum_args);
+    case 6: return sizeof(nc_sparse_rows);
   }
   return 0;
 }
@@ -687,6 +698,50 @@ int nc_frustum_mask(const nc_frustum_args* a, void* stream) {
   if (a->H > 32767 || a->W > 32767) return fail(-1, "nicecore: cv2.remap semantics need H, W < 32768");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return check_hip(timed(KID_FRUSTUM, s, [&] { return launch_frustum_mask(*a, s); }), "k_frustum_mask");
+}
+
+static int rows_check(const nc_sparse_rows* r, const char* what) {
+  if (!r) return fail(-1, std::string("nicecore: ") + what + " is NULL");
+  if (r->capacity < 0 || r->n_voxels < 0) return fail(-1, std::string("nicecore: ") + what + ": negative size");
+  if (!r->row_count || (r->capacity > 0 && (!r->grad_rows || !r->row_voxel)))
+    return fail(-1, std::string("nicecore: ") + what + ": NULL map, row_voxel or row_count");
+  if (r->capacity > INT32_MAX || r->n_voxels > INT32_MAX)
+    return fail(-1, std::string("nicecore: ") + what + ": sparse rows need < 2^31 voxels and rows");
+  return 0;
+}
+
+int nc_sparse_rows_clear(const nc_sparse_rows* r, void* stream) {
+  if (int e = rows_check(r, "rows")) return e;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_ROWS_CLEAR, s, [&] { return launch_rows_clear(*r, s); }), "k_rows_clear");
+}
+
+size_t nc_sparse_merge_temp_bytes(int64_t n_keys, int64_t n_voxels) {
+  if (n_keys < 0 || n_voxels < 0 || n_keys > INT32_MAX) return 0;
+  return rows_merge_temp_bytes(n_keys, n_voxels);
+}
+
+int nc_sparse_rows_merge(const nc_sparse_rows* in, const nc_sparse_rows* out, const int64_t* all_voxel,
+                         const int32_t* all_count, int32_t world, int64_t rank_capacity, void* temp,
+                         size_t temp_bytes, void* stream) {
+  if (int e = rows_check(in, "in")) return e;
+  if (int e = rows_check(out, "out")) return e;
+  if (in->grad_rows != out->grad_rows || in->n_voxels != out->n_voxels)
+    return fail(-1, "nicecore: merge in / out must share one voxel -> row map");
+  if (world < 1 || rank_capacity < 0 || (int64_t)world * rank_capacity > INT32_MAX)
+    return fail(-1, "nicecore: merge needs world >= 1 and world * rank_capacity < 2^31");
+  if (in->row_voxel == out->row_voxel || (in->values && in->values == out->values))
+    return fail(-1, "nicecore: merge writes new rows: out buffers must differ from in");
+  const int64_t n = (int64_t)world * rank_capacity;
+  if (n > 0 && (!all_voxel || !all_count || !out->values || !in->values))
+    return fail(-1, "nicecore: merge needs all_voxel, all_count and both value buffers");
+  if (n > 0 && (!temp || temp_bytes < nc_sparse_merge_temp_bytes(n, in->n_voxels)))
+    return fail(-1, "nicecore: merge scratch too small (nc_sparse_merge_temp_bytes)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_ROWS_MERGE, s, [&] {
+                     return launch_rows_merge(*in, *out, all_voxel, all_count, world, rank_capacity, temp, temp_bytes, s);
+                   }),
+                   "sparse rows merge");
 }
 
 }  // extern "C"

@@ -79,6 +79,11 @@ __global__ void __launch_bounds__(256) k_det_reduce(const MlpCtx m, DetBufs d, i
   const nc_grid G = grid_of(m, job_of(m, j).kind);
   const uint64_t H = (uint64_t)G.dims[1], W = (uint64_t)G.dims[2];
   const int64_t x = (int64_t)(v % W), y = (int64_t)((v / W) % H), z = (int64_t)(v / (W * H));
+  if (G.grad_rows) {  // sparse gradient rows (claimed by the forward)
+    const int r = G.grad_rows[v];
+    if (r >= 0) G.grad[(int64_t)r * 32 + ch] += acc;
+    return;
+  }
   float* dst = G.grad + z * G.grad_stride[1] + y * G.grad_stride[2] + x * G.grad_stride[3] +
                (int64_t)ch * G.grad_stride[0];
   *dst = *dst + acc;

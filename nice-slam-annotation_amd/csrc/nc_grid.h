@@ -58,7 +58,8 @@ __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners&
 // instruction covers two whole, adjacent 128-B corner rows (x0 and x0+1 of one
 // (y, z): contiguous in channels-last).  Consecutive samples of a ray in the same
 // voxel cell are summed on chip (one add per corner per run); a step to a
-// face-adjacent cell carries the shared face over.
+// face-adjacent cell carries the shared face over.  Sparse gradient rows
+// (G.grad_rows): a corner's destination is its voxel's row instead of its voxel.
 constexpr int SCAT_FLOATS = 16 * 32 + 16 * 8 + 2 * 16 * 8 + 2 * 16 + 16 + 16;  // 976 (16-B multiple)
 
 __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c, const float dc[8], bool valid,
@@ -74,11 +75,20 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
     const int yb = g & 1, zb = g >> 1;
     const float wy = yb ? c.wy[1] : c.wy[0];
     const float wz = zb ? c.wz[1] : c.wz[0];
-    const int64_t base = (c.z0 + zb) * G.grad_stride[1] + (c.y0 + yb) * G.grad_stride[2] + c.x0 * G.grad_stride[3];
     Wt[i * 8 + 2 * g] = (c.wx[0] * wy) * wz;
     Wt[i * 8 + 2 * g + 1] = (c.wx[1] * wy) * wz;
-    OFF[i * 8 + 2 * g] = base;
-    OFF[i * 8 + 2 * g + 1] = base + G.grad_stride[3];
+    if (G.grad_rows) {  // sparse gradient rows: the rows the forward claimed (-1: none, skipped)
+      const int64_t v = ((c.z0 + zb) * G.dims[1] + (c.y0 + yb)) * G.dims[2] + c.x0;
+      const int k0 = 2 * g, k1 = 2 * g + 1;
+      const int r0 = ((c.inb >> k0) & 1u) ? G.grad_rows[v] : -1;
+      const int r1 = ((c.inb >> k1) & 1u) ? G.grad_rows[v + 1] : -1;
+      OFF[i * 8 + k0] = r0 < 0 ? -1 : (int64_t)r0 * 32;
+      OFF[i * 8 + k1] = r1 < 0 ? -1 : (int64_t)r1 * 32;
+    } else {
+      const int64_t base = (c.z0 + zb) * G.grad_stride[1] + (c.y0 + yb) * G.grad_stride[2] + c.x0 * G.grad_stride[3];
+      OFF[i * 8 + 2 * g] = base;
+      OFF[i * 8 + 2 * g + 1] = base + G.grad_stride[3];
+    }
   }
   if (g == 0) {
     KEY[i] = valid ? (c.x0 | (c.y0 << 21) | (c.z0 << 42)) : -1;
@@ -88,11 +98,12 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int half = lane >> 5, ch = lane & 31;
-  const int64_t chs = (int64_t)ch * G.grad_stride[0];
+  const int64_t chs = G.grad_rows ? (int64_t)ch : (int64_t)ch * G.grad_stride[0];
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   auto flush = [&](int pt, int xb, int q, float v) {
     const int k = xb | (q << 1);
-    if ((INB[pt] >> k) & 1) atomicAdd(G.grad + OFF[pt * 8 + k] + chs, v);
+    const int64_t o = OFF[pt * 8 + k];
+    if (((INB[pt] >> k) & 1) && o >= 0) atomicAdd(G.grad + o + chs, v);
   };
   int run = 0;
   int64_t cur = KEY[0];

@@ -9,6 +9,39 @@ __device__ __forceinline__ Job pick_job3(const Job (&jobs)[MAX_JOBS], unsigned y
   return y == 0 ? jobs[0] : (y == 1 ? jobs[1] : jobs[2]);
 }
 
+// Sparse gradient rows (nc_grid.grad_rows, ABI v5): the first lookup that touches an
+// in-bounds voxel claims it a gradient row -- compare-and-swap -1 -> -2 on the map
+// entry, then one counter atomic per wavefront for all of its winners -- zero-fills
+// the row and records the voxel.  The backward (nc_grid.h grid_scatter) accumulates
+// into rows[voxel].  An overflowing claim (row >= capacity) is undone (map back to
+// -1; the counter keeps the overshoot, which the caller checks).
+__device__ __forceinline__ void claim_row(const nc_grid& G, const Corners& co, int k) {
+  const bool in = (co.inb >> k) & 1u;
+  const int64_t x = co.x0 + (k & 1), y = co.y0 + ((k >> 1) & 1), z = co.z0 + (k >> 2);
+  const int64_t v = in ? (z * G.dims[1] + y) * G.dims[2] + x : 0;
+  bool won = false;
+  if (in && __hip_atomic_load(G.grad_rows + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == -1)
+    won = atomicCAS(G.grad_rows + v, -1, -2) == -1;
+  const uint64_t m = __ballot(won);
+  if (m == 0) return;
+  const int leader = __builtin_ctzll(m);
+  const int lane = __lane_id();
+  int base = 0;
+  if (lane == leader) base = atomicAdd(G.row_count, (int)__builtin_popcountll(m));
+  base = __shfl(base, leader);
+  if (!won) return;
+  const int64_t row = base + (int64_t)__builtin_popcountll(m & ((uint64_t(1) << lane) - 1));
+  if (row >= G.row_capacity) {
+    atomicExch(G.grad_rows + v, -1);
+    return;
+  }
+  G.row_voxel[row] = v;
+  float4* dst = reinterpret_cast<float4*>(G.grad + row * 32);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) dst[c] = float4{0.f, 0.f, 0.f, 0.f};
+  atomicExch(G.grad_rows + v, (int)row);
+}
+
 // ---------------------------------------------------------------------------
 // Forward trilinear lookups (MLP.sample_grid_feature, decoder.py:179-188, and the
 // fine decoder's no-grad grid_middle lookup, :196-202) for every (point, job), as
@@ -68,6 +101,8 @@ __global__ void __launch_bounds__(256) k_grid_gather(const MlpCtx ctx) {
     o.w = o.w + (in ? v[k].w * w : 0.f);
   }
   *reinterpret_cast<float4*>(ctx.cfeat + job.c_off + p * job.c_stride + 4 * q) = o;
+  if (ctx.claim_rows && q < 8 && G.grad_rows)  // sparse gradient rows: lane q claims corner q
+    claim_row(G, co, q);
   if (ctx.share_mid && y == 1)  // the fine decoder's no-grad grid_middle lookup is this one
     *reinterpret_cast<float4*>(ctx.cfeat + ctx.jobs[0].c_off + p * ctx.jobs[0].c_stride + 32 + 4 * q) = o;
   if (ctx.zero_fill) {

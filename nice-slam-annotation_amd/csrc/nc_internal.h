@@ -53,6 +53,8 @@ struct MlpCtx {
                                   // (both split in proportion to the decoders' per-point MACs)
   float4* zero_fill;         // optional: k_grid_gather also zero-fills zero_n4 float4s here (the
   int64_t zero_n4;           // caller's gradient buffer, nc_render_args.grad_zero)
+  int32_t claim_rows;        // forward for a backward: k_grid_gather claims sparse gradient rows
+                             // (nc_grid.grad_rows) of the grids that have a row map
   float* dfeat;              // NC_DETERMINISTIC: [n_jobs][P][32] d features of each job's own grid
                              // (k_mlp_dx stores them instead of scattering with atomics), else NULL
 };
@@ -78,6 +80,12 @@ int launch_sample_rays(const nc_sample_args& a, hipStream_t s);
 int launch_sample_pose_grad(const nc_sample_args& a, hipStream_t s);
 // frustum feature selection (nc_frustum.hip)
 int launch_frustum_mask(const nc_frustum_args& a, hipStream_t s);
+// sparse gradient rows (nc_sparse.hip)
+int launch_rows_clear(const nc_sparse_rows& r, hipStream_t s);
+size_t rows_merge_temp_bytes(int64_t n_keys, int64_t n_voxels);
+int launch_rows_merge(const nc_sparse_rows& in, const nc_sparse_rows& out, const int64_t* all_voxel,
+                      const int32_t* all_count, int world, int64_t rank_capacity, void* temp, size_t temp_bytes,
+                      hipStream_t s);
 
 // Arguments of the per-ray kernels (sampling, compositing, ray gradients).
 struct RayCtx {

@@ -1,0 +1,168 @@
+// nc_sparse.hip -- sparse (touched-voxel) gradient rows of a feature grid (ABI v5).
+//
+// The reference's grid gradient is dense: autograd's grid.grad (Mapper.py:620-627
+// steps Adam on the frustum-selected val[mask], Mapper.py:392-404).  For a grid of
+// 200M voxels (BASELINE configs[4], 26 GB) a dense gradient costs a 26 GB zero fill
+// and, over 8 ranks, a 26 GB all-reduce per iteration, while one batch touches at
+// most 8 corners per lookup.  With nc_grid.grad_rows the forward claims one
+// gradient row per touched voxel (k_grid_gather, nc_grid.hip) and the backward
+// accumulates into the rows (nc_grid.h); this file holds the rest:
+//   k_rows_clear      map entries of the claimed rows back to -1, counter to 0
+//   merge             the union of every rank's touched voxels, ascending:
+//     k_merge_keys      rank r's voxels (i < count[r]) or a sentinel
+//     radix sort        rocprim radix_sort_keys over the voxel bits
+//     k_merge_heads     1 at the first key of each distinct voxel
+//     inclusive scan    rocprim inclusive_scan of the head flags -> row of each key
+//     k_merge_rows      the union's row_voxel, the map re-pointed, rows zeroed
+//     k_merge_permute   this rank's gradient rows copied to their union rows
+// after which every rank holds the same rows in the same order and one RCCL sum
+// over rows [0, count) reduces the sparse gradient.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "nc_internal.h"
+
+namespace nc {
+
+__global__ void __launch_bounds__(256) k_rows_clear(nc_sparse_rows r) {
+  const int64_t n = min((int64_t)*r.row_count, r.capacity);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    r.grad_rows[r.row_voxel[i]] = -1;
+}
+
+__global__ void k_rows_count_zero(int32_t* c) { *c = 0; }
+
+int launch_rows_clear(const nc_sparse_rows& r, hipStream_t s) {
+  if (r.capacity > 0) {
+    // the claimed-row count lives on the device: enough workgroups for a full buffer,
+    // each strides over whatever is claimed
+    const int64_t blocks = std::min<int64_t>((r.capacity + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_rows_clear, dim3((unsigned)blocks), dim3(256), 0, s, r);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  hipLaunchKernelGGL(k_rows_count_zero, dim3(1), dim3(1), 0, s, r.row_count);
+  return (int)hipGetLastError();
+}
+
+struct MergeBufs {
+  uint64_t* key[2];  // [n] unsorted / sorted voxel keys
+  int32_t* head;     // [n] 1 at the first key of a voxel
+  int32_t* row;      // [n] inclusive scan of head: row + 1 of each key
+  void* temp;        // rocprim scratch (sort and scan share it)
+  size_t temp_bytes;
+};
+
+static int voxel_bits(int64_t n_voxels) {
+  int b = 1;
+  while ((int64_t(1) << b) <= n_voxels) ++b;  // sentinel 2^b - 1 > every voxel index
+  return b;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+static size_t rocprim_temp(int64_t n, int bits) {
+  size_t sort_bytes = 0, scan_bytes = 0;
+  if (rocprim::radix_sort_keys(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, 0,
+                               (unsigned)bits) != hipSuccess)
+    return 0;
+  if (rocprim::inclusive_scan(nullptr, scan_bytes, (int32_t*)nullptr, (int32_t*)nullptr, (size_t)n,
+                              rocprim::plus<int32_t>()) != hipSuccess)
+    return 0;
+  return std::max<size_t>(std::max(sort_bytes, scan_bytes), 1);
+}
+
+size_t rows_merge_temp_bytes(int64_t n_keys, int64_t n_voxels) {
+  if (n_keys <= 0) return 256;
+  const size_t t = rocprim_temp(n_keys, voxel_bits(n_voxels));
+  if (t == 0) return 0;
+  return 2 * align256(n_keys * sizeof(uint64_t)) + 2 * align256(n_keys * sizeof(int32_t)) + align256(t);
+}
+
+__global__ void __launch_bounds__(256) k_merge_keys(const int64_t* all_voxel, const int32_t* all_count,
+                                                    int64_t rank_capacity, int64_t n, uint64_t sentinel,
+                                                    uint64_t* key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = i / rank_capacity, j = i - r * rank_capacity;
+  const int64_t cnt = min((int64_t)all_count[r], rank_capacity);
+  key[i] = j < cnt ? (uint64_t)all_voxel[i] : sentinel;
+}
+
+__global__ void __launch_bounds__(256) k_merge_heads(const uint64_t* key, int64_t n, uint64_t sentinel,
+                                                     int32_t* head) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = key[i];
+  head[i] = (k != sentinel && (i == 0 || key[i - 1] != k)) ? 1 : 0;
+}
+
+// key i that heads its voxel run gets row row[i] - 1; the last scan value is the
+// union's size.  Rows beyond out.capacity are dropped and flagged by the count.
+__global__ void __launch_bounds__(256) k_merge_rows(const uint64_t* key, const int32_t* head, const int32_t* row,
+                                                    int64_t n, nc_sparse_rows out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *out.row_count = n > 0 ? row[n - 1] : 0;
+  if (i >= n || !head[i]) return;
+  const int64_t r = row[i] - 1;
+  if (r >= out.capacity) return;
+  const int64_t v = (int64_t)key[i];
+  out.row_voxel[r] = v;
+  out.grad_rows[v] = (int32_t)r;
+  float4* dst = reinterpret_cast<float4*>(out.values + r * 32);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) dst[c] = float4{0.f, 0.f, 0.f, 0.f};
+}
+
+// thread = (local row, 4-channel chunk): this rank's row -> the union row of its voxel
+__global__ void __launch_bounds__(256) k_merge_permute(nc_sparse_rows in, nc_sparse_rows out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = t >> 3;
+  const int c = (int)(t & 7);
+  const int64_t n = min((int64_t)*in.row_count, in.capacity);
+  if (i >= n) return;
+  const int32_t r = out.grad_rows[in.row_voxel[i]];
+  if (r < 0 || r >= out.capacity) return;
+  reinterpret_cast<float4*>(out.values + (int64_t)r * 32)[c] =
+      reinterpret_cast<const float4*>(in.values + i * 32)[c];
+}
+
+int launch_rows_merge(const nc_sparse_rows& in, const nc_sparse_rows& out, const int64_t* all_voxel,
+                      const int32_t* all_count, int world, int64_t rank_capacity, void* temp, size_t temp_bytes,
+                      hipStream_t s) {
+  const int64_t n = (int64_t)world * rank_capacity;
+  if (n == 0) {
+    hipLaunchKernelGGL(k_rows_count_zero, dim3(1), dim3(1), 0, s, out.row_count);
+    return (int)hipGetLastError();
+  }
+  const int bits = voxel_bits(in.n_voxels);
+  const uint64_t sentinel = (uint64_t(1) << bits) - 1;
+  char* p = static_cast<char*>(temp);
+  MergeBufs b;
+  b.key[0] = reinterpret_cast<uint64_t*>(p); p += align256(n * sizeof(uint64_t));
+  b.key[1] = reinterpret_cast<uint64_t*>(p); p += align256(n * sizeof(uint64_t));
+  b.head = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
+  b.row = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
+  b.temp = p;
+  b.temp_bytes = temp_bytes - (size_t)(p - static_cast<char*>(temp));
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_merge_keys, dim3(blocks), dim3(256), 0, s, all_voxel, all_count, rank_capacity, n, sentinel,
+                     b.key[0]);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  size_t tb = b.temp_bytes;
+  if (hipError_t e = rocprim::radix_sort_keys(b.temp, tb, b.key[0], b.key[1], (size_t)n, 0, (unsigned)bits, s))
+    return (int)e;
+  hipLaunchKernelGGL(k_merge_heads, dim3(blocks), dim3(256), 0, s, b.key[1], n, sentinel, b.head);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  tb = b.temp_bytes;
+  if (hipError_t e = rocprim::inclusive_scan(b.temp, tb, b.head, b.row, (size_t)n, rocprim::plus<int32_t>(), s))
+    return (int)e;
+  hipLaunchKernelGGL(k_merge_rows, dim3(blocks), dim3(256), 0, s, b.key[1], b.head, b.row, n, out);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  const int64_t pt = in.capacity * 8;
+  if (pt > 0)
+    hipLaunchKernelGGL(k_merge_permute, dim3((unsigned)((pt + 255) / 256)), dim3(256), 0, s, in, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace nc

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 4
+NC_ABI_VERSION = 5
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
 NC_LOSS_NONE, NC_LOSS_MAPPER, NC_LOSS_TRACKER = 0, 1, 2
@@ -33,7 +33,9 @@ STAGE_GRIDS = {0: (0,), 1: (1,), 2: (1, 2), 3: (1, 2, 3)}
 
 class NcGrid(ctypes.Structure):
     _fields_ = [("data", c_void_p), ("grad", c_void_p), ("dims", c_int64 * 3),
-                ("stride", c_int64 * 4), ("grad_stride", c_int64 * 4)]
+                ("stride", c_int64 * 4), ("grad_stride", c_int64 * 4),
+                ("grad_rows", c_void_p), ("row_voxel", c_void_p), ("row_count", c_void_p),
+                ("row_capacity", c_int64)]
 
 
 class NcDecoderParams(ctypes.Structure):
@@ -87,6 +89,11 @@ class NcFrustumArgs(ctypes.Structure):
                 ("mask", c_void_p), ("scratch", c_void_p)]
 
 
+class NcSparseRows(ctypes.Structure):
+    _fields_ = [("grad_rows", c_void_p), ("n_voxels", c_int64), ("row_voxel", c_void_p),
+                ("row_count", c_void_p), ("capacity", c_int64), ("values", c_void_p)]
+
+
 EXPORTS = {
     "nc_abi_version": (c_int, []),
     "nc_last_error": (ctypes.c_char_p, []),
@@ -104,6 +111,10 @@ EXPORTS = {
     "nc_sample_rays_forward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
     "nc_sample_rays_backward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
     "nc_frustum_mask": (c_int, [POINTER(NcFrustumArgs), c_void_p]),
+    "nc_sparse_rows_clear": (c_int, [POINTER(NcSparseRows), c_void_p]),
+    "nc_sparse_merge_temp_bytes": (c_size_t, [c_int64, c_int64]),
+    "nc_sparse_rows_merge": (c_int, [POINTER(NcSparseRows), POINTER(NcSparseRows), c_void_p, c_void_p,
+                                     c_int32, c_int64, c_void_p, c_size_t, c_void_p]),
 }
 
 _lib = None
@@ -144,7 +155,8 @@ KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_f
               "k_composite_bwd": 4, "k_mlp_dx": 5, "k_param_reduce": 6, "k_ray_grads": 7,
               "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10,
               "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15,
-              "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18}
+              "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18,
+              "k_rows_clear": 19, "k_rows_merge": 20}
 
 
 class KernelTimer:

@@ -11,17 +11,18 @@ def _grid_args(c):
     return [c.get(k) if c is not None else None for k in L.GRID_KEYS]
 
 
-def eval_points(decoders, p, c_grid, stage='middle', deterministic=None):
+def eval_points(decoders, p, c_grid, stage='middle', deterministic=None, sparse_grads=None):
     """NICE.forward(p, c_grid, stage) (src/conv_onet/models/decoder.py:336-370):
     raw [P,4] float32 for points p ([P,3] or [1,P,3]); differentiable w.r.t. p,
-    the grids and the decoder parameters.  ``deterministic``: see render_rays."""
+    the grids and the decoder parameters.  ``deterministic``, ``sparse_grads``: see
+    render_rays."""
     plan = make_plan(stage, decoders)
-    spec = {"plan": plan, "deterministic": deterministic}
+    spec = {"plan": plan, "deterministic": deterministic, "sparse": sparse_grads}
     return NiceEvalFn.apply(spec, p, *_grid_args(c_grid), *plan.flat_params())
 
 
 def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_strat=32,
-                n_surf=16, depth_max=None, deterministic=None):
+                n_surf=16, depth_max=None, deterministic=None, sparse_grads=None):
     """Renderer.render_batch_ray core (src/utils/Renderer.py:95-262) with
     N_importance = 0, lindisp = False, perturb = 0, occupancy = True.
     Returns (depth float64 [N], uncertainty float64 [N], color float32 [N,3]).
@@ -31,7 +32,10 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
 
     ``deterministic``: grid gradients by an ordered per-voxel reduction (bit-identical
     run to run) instead of float atomics; None = the environment variable
-    ``NC_DETERMINISTIC=1`` or ``torch.use_deterministic_algorithms(True)``."""
+    ``NC_DETERMINISTIC=1`` or ``torch.use_deterministic_algorithms(True)``.
+
+    ``sparse_grads``: a ``nicecore.sparse.SparseGridGrads``; the grids it covers get
+    their gradient as touched-voxel rows there instead of a dense ``.grad``."""
     if stage == 'coarse':
         gt_depth = None
     ns = n_surf if gt_depth is not None else 0
@@ -39,7 +43,7 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
         raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
-            "deterministic": deterministic}
+            "deterministic": deterministic, "sparse": sparse_grads}
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
 
 
@@ -48,7 +52,8 @@ _LOSS_KINDS = {"mapper": L.NC_LOSS_MAPPER, "tracker": L.NC_LOSS_TRACKER}
 
 def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, loss="mapper",
                      target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
-                     gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None):
+                     gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None,
+                     sparse_grads=None):
     """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
     color, loss) with ``loss`` a float64 device scalar that backpropagates into the
     grids / decoders / rays like the reference's loss expression:
@@ -80,6 +85,6 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
         raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
-            "deterministic": deterministic, "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth,
-                     target_color if color_term else None)}
+            "deterministic": deterministic, "sparse": sparse_grads,
+            "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth, target_color if color_term else None)}
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())

@@ -273,6 +273,27 @@ def _dense_strides(g):
     return (C * D * H * W, D * H * W, H * W, W, 1)
 
 
+def _dense_needs(needs_grids, sparse):
+    """needs_input_grad of the grids minus those whose gradient goes to sparse rows."""
+    if sparse is None:
+        return needs_grids
+    return tuple(bool(n) and not sparse.covers(k) for k, n in enumerate(needs_grids))
+
+
+def _bind_sparse(sparse, args, plan, n_points=None):
+    """Point the grids that have sparse gradient rows at them (nicecore.sparse): the
+    forward (n_points given) reserves room for its claims, the backward re-binds the
+    current buffers (a later forward may have grown them)."""
+    if sparse is None:
+        return
+    for k in plan.grids:
+        if sparse.covers(k):
+            if n_points is None:
+                sparse.bind_backward(args.grids[k], k)
+            else:
+                sparse.bind_forward(args.grids[k], k, n_points)
+
+
 def _grad_sizes(lib, plan, needs_params, needs_grids, grids):
     sl = plan.param_slices()
     gk = [k for k in plan.grids if needs_grids[k]]
@@ -282,7 +303,7 @@ def _grad_sizes(lib, plan, needs_params, needs_grids, grids):
     return gk, pk, gsize, psize
 
 
-def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device, prezeroed=None):
+def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device, prezeroed=None, sparse=None):
     """Every gradient of one backward call lives in ONE float32 buffer: the grid
     gradients first (strided views with each grid's own memory format, zero-filled
     by a single kernel), then one flat parameter vector per decoder whose
@@ -301,6 +322,8 @@ def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device, prez
     off = 0
     for k in plan.grids:
         args.grids[k].grad = None
+        args.grids[k].grad_rows = None
+    _bind_sparse(sparse, args, plan)
     for k in gk:
         g = grids[k]
         gg = torch.as_strided(buf, g.shape, _dense_strides(g), off)
@@ -348,6 +371,7 @@ class NiceRenderFn(torch.autograd.Function):
     def forward(ctx, spec, rays_o, rays_d, gt_depth, g0, g1, g2, g3, *params):
         lib = L.load()
         plan = spec["plan"]
+        sparse = spec.get("sparse")
         device = rays_o.device
         if device.type != "cuda":
             raise L.NiceCoreError("nicecore renders on a HIP device; tensors are on " + str(device))
@@ -377,6 +401,8 @@ class NiceRenderFn(torch.autograd.Function):
             g = grids[k].detach()
             _fill_grid(a.grids[k], g, device)
             gkeep.append(g)
+        if a.flags & L.NC_SAVE_FOR_BACKWARD:
+            _bind_sparse(sparse, a, plan, N * (spec["n_strat"] + spec["n_surf"]))
         depth = torch.empty(N, device=device, dtype=torch.float64)
         var = torch.empty(N, device=device, dtype=torch.float64)
         color = torch.empty(N, 3, device=device, dtype=torch.float32)
@@ -395,9 +421,9 @@ class NiceRenderFn(torch.autograd.Function):
         # the backward's gradient buffer: allocated here and zero-filled by the forward's
         # gather kernel (no separate fill launch); used by the first backward call
         ctx.grad_buf = None
-        if _FWD_ZERO and any(ctx.needs_input_grad[4:8]):
-            _, _, gsize, psize = _grad_sizes(lib, plan, ctx.needs_input_grad[8:], ctx.needs_input_grad[4:8],
-                                             (g0, g1, g2, g3))
+        dneeds = _dense_needs(ctx.needs_input_grad[4:8], sparse)
+        if _FWD_ZERO and any(dneeds):
+            _, _, gsize, psize = _grad_sizes(lib, plan, ctx.needs_input_grad[8:], dneeds, (g0, g1, g2, g3))
             if gsize:
                 ctx.grad_buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
                 a.grad_zero, a.grad_zero_floats = ctx.grad_buf.data_ptr(), gsize
@@ -409,6 +435,7 @@ class NiceRenderFn(torch.autograd.Function):
         L.check(lib.nc_render_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_render_forward")
         a.grad_zero, a.grad_zero_floats = None, 0
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
+        ctx.sparse = sparse
         ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt)
         ctx.grids = grids
         if loss is None:
@@ -436,8 +463,8 @@ class NiceRenderFn(torch.autograd.Function):
             g_rd = g_rd if g_rd is not None else torch.empty_like(rays_o)
         a.g_rays_o, a.g_rays_d = _ptr(g_ro), _ptr(g_rd)
         needs_params = need[8:]
-        grid_grads, flats = _alloc_grads(lib, plan, needs_params, need[4:8], ctx.grids, a, device,
-                                         prezeroed=ctx.grad_buf)
+        grid_grads, flats = _alloc_grads(lib, plan, needs_params, _dense_needs(need[4:8], ctx.sparse), ctx.grids,
+                                         a, device, prezeroed=ctx.grad_buf, sparse=ctx.sparse)
         ctx.grad_buf = None  # a second backward (retain_graph) gets a fresh, zeroed buffer
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_render_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
@@ -453,6 +480,7 @@ class NiceEvalFn(torch.autograd.Function):
     def forward(ctx, spec, p, g0, g1, g2, g3, *params):
         lib = L.load()
         plan = spec["plan"]
+        sparse = spec.get("sparse")
         device = p.device
         if device.type != "cuda":
             raise L.NiceCoreError("nicecore evaluates on a HIP device; points are on " + str(device))
@@ -470,6 +498,8 @@ class NiceEvalFn(torch.autograd.Function):
             g = grids[k].detach()
             _fill_grid(a.grids[k], g, device)
             gkeep.append(g)
+        if a.flags & L.NC_SAVE_FOR_BACKWARD:
+            _bind_sparse(sparse, a, plan, P)
         raw = torch.empty(P, 4, device=device, dtype=torch.float32)
         a.raw = raw.data_ptr()
         nbytes = lib.nc_points_workspace_bytes(ctypes.byref(a))
@@ -477,6 +507,7 @@ class NiceEvalFn(torch.autograd.Function):
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_points_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_points_forward")
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
+        ctx.sparse = sparse
         ctx.keep = (pts, gkeep, params)
         ctx.grids = grids
         ctx.p_dtype, ctx.p_shape = p.dtype, p.shape
@@ -494,7 +525,8 @@ class NiceEvalFn(torch.autograd.Function):
         g_pts = torch.empty_like(pts) if need[1] else None
         a.g_pts = _ptr(g_pts)
         needs_params = need[6:]
-        grid_grads, flats = _alloc_grads(lib, plan, needs_params, need[2:6], ctx.grids, a, device)
+        grid_grads, flats = _alloc_grads(lib, plan, needs_params, _dense_needs(need[2:6], ctx.sparse), ctx.grids,
+                                         a, device, sparse=ctx.sparse)
         stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_points_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
                 "nc_points_backward")

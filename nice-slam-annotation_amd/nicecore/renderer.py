@@ -65,18 +65,20 @@ class Renderer(object):
         return torch.cat(outs, dim=0)
 
     def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None,
-                         depth_max=None):
-        """Renderer.py:95-262.  ``depth_max`` (extension) overrides the batch-global
-        max(gt_depth) with a precomputed (e.g. all-reduced) device scalar."""
+                         depth_max=None, sparse_grads=None):
+        """Renderer.py:95-262.  Extensions: ``depth_max`` overrides the batch-global
+        max(gt_depth) with a precomputed (e.g. all-reduced) device scalar;
+        ``sparse_grads`` (nicecore.sparse.SparseGridGrads) takes the covered grids'
+        gradients as touched-voxel rows (grids too large for a dense gradient)."""
         self._check_supported()
         if gt_depth is not None:
             gt_depth = gt_depth.reshape(-1)
         return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
-                           self.N_samples, self.N_surface, depth_max)
+                           self.N_samples, self.N_surface, depth_max, sparse_grads=sparse_grads)
 
     def render_batch_loss(self, c, decoders, rays_d, rays_o, device, stage, gt_depth, gt_color=None,
                           loss='mapper', w_color_loss=0.2, color_term=False, handle_dynamic=False,
-                          render_gt_depth='target', depth_max=None):
+                          render_gt_depth='target', depth_max=None, sparse_grads=None):
         """render_batch_ray + the rendering loss (ops.render_rays_loss): returns
         (depth, uncertainty, color, loss).  Mapper.optimize_map:
         ``loss='mapper', color_term=(not nice) or stage == 'color',
@@ -85,7 +87,8 @@ class Renderer(object):
         self._check_supported()
         return render_rays_loss(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth.reshape(-1),
                                 loss, gt_color, w_color_loss, color_term, handle_dynamic,
-                                render_gt_depth, self.N_samples, self.N_surface, depth_max)
+                                render_gt_depth, self.N_samples, self.N_surface, depth_max,
+                                sparse_grads=sparse_grads)
 
     def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
         """Renderer.py:264-340: chunked full-image render, no grad."""
