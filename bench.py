@@ -196,7 +196,14 @@ def algorithmic_flops_per_ray(stage, S, mode):
     fwd = 2 * sum(MAC[d] for d in decs) + TRI_FLOP * lk_fwd
     dx = 2 * sum(MAC_DX[d] for d in decs)
     dw = 2 * sum(MAC[d] for d in decs) if mode == "ba" else 0
-    return {"k_mlp_fwd": fwd * S, "k_mlp_dx": dx * S, "k_mlp_dw": dw * S}
+    return {"k_mlp_fwd": fwd * S, "k_mlp_dx": dx * S, "k_mlp_dw": dw * S,
+            "k_grid_gather": TRI_FLOP * LOOKUPS_UNIQUE[stage] * S}
+
+
+# distinct trilinear lookups per point (k_grid_gather reads grid_middle once for the fine
+# and middle decoders, MlpCtx::share_mid); lk_fwd of them are written out
+LOOKUPS_UNIQUE = {"coarse": 1, "middle": 1, "fine": 2, "color": 3}
+LOOKUPS_FWD = {"coarse": 1, "middle": 1, "fine": 3, "color": 4}
 
 
 # point-record geometry of the core (csrc/nc_mlp.hip Rec<KIND>): floats per point
@@ -212,9 +219,18 @@ def algorithmic_bytes_per_point(stage, mode):
     decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
             "color": ["fine", "middle", "color"]}[stage]
     fwd = sum(4 * FEAT[d] + 16 + 4 * (REC_LEN[d] - FEAT[d]) + 4 * NOUT[d] for d in decs)
-    dx = sum(32 + 4 * NOUT[d] + 16 + 4 * (REC_STRIDE[d] - REC_LEN[d]) + 128 + 24 for d in decs)
+    # k_mlp_dx per decoder: masks 32 B + d out + p.float() 16 B + normalised xyz 16 B in,
+    # point gradient 24 B out, the saved trilinear Jacobian 384 B in (NC_SAVE_POINT_JACOBIAN);
+    # BA mode adds the backward record out and the grid-gradient scatter, counted as
+    # SURVEY.md §8(d) does: 2 x 1,024 B (read-modify-write of 8 corner rows) per lookup
+    ba = mode == "ba"
+    dx = sum(32 + 4 * NOUT[d] + 16 + 16 + 24 + 384 +
+             ((4 * (REC_STRIDE[d] - REC_LEN[d]) + 2 * 1024) if ba else 0) for d in decs)
     dw = sum(4 * REC_STRIDE[d] for d in decs) if mode == "ba" else 0
-    return {"k_mlp_fwd": fwd, "k_mlp_dx": dx, "k_mlp_dw": dw}
+    # k_grid_gather: 8 corner rows of 128 B per distinct lookup, 128 B of features out per
+    # lookup, and the 384-B trilinear Jacobian of each decoder's own lookup (ray gradients)
+    gather = 1024 * LOOKUPS_UNIQUE[stage] + 128 * LOOKUPS_FWD[stage] + 384 * len(decs)
+    return {"k_mlp_fwd": fwd, "k_mlp_dx": dx, "k_mlp_dw": dw, "k_grid_gather": gather}
 
 
 def cpu_baseline(args, seconds):
@@ -343,7 +359,7 @@ def main():
                       f"eagerly just before the graph-replay timed region")
     avg_ms = ms_dom / max(n_dom, 1)
 
-    S = 48
+    S = 32 if args.stage == "coarse" else 48  # the coarse mapper renders without gt depth (Mapper.py:600)
     per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode)
     per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode)
     fl = per_ray[dominant] * args.rays if dominant in per_ray else None

@@ -62,6 +62,12 @@ extern "C" {
  * to run, summed per voxel in the reference's order (ascending point, corner).  Set it
  * on the forward (it sizes the workspace) and keep it for the backward. */
 #define NC_DETERMINISTIC 2
+/* The backward will ask for ray / point gradients (ABI v5): the forward then also keeps
+ * each decoder lookup's trilinear Jacobian d features / d (ix, iy, iz) (3 x 32 floats
+ * per point, from the corner values it gathers anyway), and the backward's coordinate
+ * gradient is 96 multiply-adds per point instead of 8 corner re-reads.  Without it a
+ * backward with g_rays_* / g_pts re-reads the corners. */
+#define NC_SAVE_POINT_JACOBIAN 4
 
 /* nc_render_args.loss: the rendering loss computed by the core (optional) */
 #define NC_LOSS_NONE 0

@@ -162,6 +162,8 @@ struct Ws {
          coef_d = 0, coef_c = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dtemp = 0, dtemp_bytes = 0,
          total = 0;
   bool det = false;
+  size_t jac = 0;
+  bool has_jac = false;
   int vbits = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
@@ -189,7 +191,8 @@ void split_wgs(int total, int64_t blocks, const Job* jobs, int n_jobs, int32_t* 
   for (int j = n_jobs + 1; j <= MAX_JOBS; ++j) off[j] = off[n_jobs];
 }
 
-void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1) {
+void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1,
+            bool jac = false) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -206,6 +209,8 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
   w.gocc = take((size_t)P * 4);
   w.grgb = take((size_t)P * 12);
   w.dpts = take((size_t)pl.n_jobs * P * 24);
+  w.jac = (save && jac) ? take((size_t)pl.n_jobs * P * 96 * 4) : 0;
+  w.has_jac = save && jac;
   if (loss) {  // per-ray loss derivatives, forward -> backward
     w.coef_d = take((size_t)N * 8);
     w.coef_c = take((size_t)N * 12);
@@ -299,6 +304,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.cfeat = w.save ? m.rec : at<float>(ws, w.feat);
   m.claim_rows = w.save;  // only grids with a row map (nc_grid.grad_rows) claim
   m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
+  m.jac = w.has_jac ? at<float>(ws, w.jac) : nullptr;
 }
 
 DetBufs det_bufs(void* ws, const Ws& w) {
@@ -338,7 +344,7 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
   S = a->n_strat + a->n_surf;
   P = a->n_rays * S;
-  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC)) return fail(-1, "nicecore: unknown flags");
+  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC | NC_SAVE_POINT_JACOBIAN)) return fail(-1, "nicecore: unknown flags");
   if (a->loss < NC_LOSS_NONE || a->loss > NC_LOSS_TRACKER) return fail(-1, "nicecore: unknown loss " + std::to_string(a->loss));
   if (a->loss != NC_LOSS_NONE) {
     if (a->loss_flags & ~(NC_LOSS_COLOR | NC_LOSS_DYNAMIC)) return fail(-1, "nicecore: unknown loss_flags");
@@ -356,7 +362,8 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
     if (vbits > 60 || (int64_t)pl.n_jobs * P * 8 >= (int64_t(1) << 32))
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
-  layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w, vbits);
+  layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w, vbits,
+         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0);
   if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }
@@ -602,14 +609,15 @@ static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
   if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
   if (int e = plan_stage(a->stage, pl)) return e;
   if (a->n_points < 0) return fail(-1, "nicecore: n_points < 0");
-  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC)) return fail(-1, "nicecore: unknown flags");
+  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC | NC_SAVE_POINT_JACOBIAN)) return fail(-1, "nicecore: unknown flags");
   int vbits = -1;
   if (a->flags & NC_DETERMINISTIC) {
     vbits = stage_vbits(pl, a->grids);
     if (vbits > 60 || (int64_t)pl.n_jobs * a->n_points * 8 >= (int64_t(1) << 32))
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
-  layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w, vbits);
+  layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w, vbits,
+         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0);
   if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }

@@ -24,7 +24,13 @@ __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners&
     float v[4][8];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      const float* base = G.data + c.off[4 * h + kk];
+      // corner offset from the corner-0 voxel (not Corners::off: 16 fewer live VGPRs
+      // across the decoder backward); out-of-bounds corners read cell 0
+      const int k = 4 * h + kk;
+      const bool in = (c.inb >> k) & 1u;
+      const int64_t o = (c.z0 + (k >> 2)) * G.stride[1] + (c.y0 + ((k >> 1) & 1)) * G.stride[2] +
+                        (c.x0 + (k & 1)) * G.stride[3];
+      const float* base = G.data + (in ? o : 0);
       if (VEC) {
         const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
         const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
@@ -60,49 +66,65 @@ __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners&
 // voxel cell are summed on chip (one add per corner per run); a step to a
 // face-adjacent cell carries the shared face over.  Sparse gradient rows
 // (G.grad_rows): a corner's destination is its voxel's row instead of its voxel.
-constexpr int SCAT_FLOATS = 16 * 32 + 16 * 8 + 2 * 16 * 8 + 2 * 16 + 16 + 16;  // 976 (16-B multiple)
+// Slice layout (floats), padded so the per-lane writes of the 16 points spread over
+// the LDS banks: D [16][36] (row pad 4), Wt / OFF transposed [corner][17].
+constexpr int SCAT_DLD = 36, SCAT_KLD = 17;
+constexpr int SCAT_WT = 16 * SCAT_DLD;             // 576
+constexpr int SCAT_OFF = SCAT_WT + 8 * SCAT_KLD;   // 712 (8-B aligned)
+constexpr int SCAT_KEY = SCAT_OFF + 2 * 8 * SCAT_KLD;  // 984
+constexpr int SCAT_INB = SCAT_KEY + 2 * 16;        // 1016
+constexpr int SCAT_FLOATS = SCAT_INB + 16;         // 1032 (16-B multiple)
+static_assert(SCAT_FLOATS % 4 == 0 && SCAT_OFF % 2 == 0 && SCAT_KEY % 2 == 0, "scatter slice alignment");
 
-__device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c, const float dc[8], bool valid,
-                                             float* reg, int i, int g, int lane) {
-  float* D = reg;                                           // [16][32] d features
-  float* Wt = reg + 512;                                    // [16][8] corner weights
-  int64_t* OFF = reinterpret_cast<int64_t*>(reg + 640);     // [16][8] grad-corner offsets
-  int64_t* KEY = reinterpret_cast<int64_t*>(reg + 896);     // [16] voxel-cell key (-1: none)
-  int* INB = reinterpret_cast<int*>(reg + 928);             // [16] in-bounds corner mask
-  *reinterpret_cast<float4*>(D + i * 32 + 4 * g) = float4{dc[0], dc[1], dc[2], dc[3]};
-  *reinterpret_cast<float4*>(D + i * 32 + 16 + 4 * g) = float4{dc[4], dc[5], dc[6], dc[7]};
+// (1) staging: every lane of the wave that owns the 16 points writes its share
+__device__ __forceinline__ void grid_scatter_stage(const nc_grid& G, const Corners& c, const float dc[8], bool valid,
+                                                   float* reg, int i, int g) {
+  float* D = reg;                                              // [16][36] d features
+  float* Wt = reg + SCAT_WT;                                   // [8][17] corner weights
+  int64_t* OFF = reinterpret_cast<int64_t*>(reg + SCAT_OFF);   // [8][17] grad-corner offsets
+  int64_t* KEY = reinterpret_cast<int64_t*>(reg + SCAT_KEY);   // [16] voxel-cell key (-1: none)
+  int* INB = reinterpret_cast<int*>(reg + SCAT_INB);           // [16] in-bounds corner mask
+  *reinterpret_cast<float4*>(D + i * SCAT_DLD + 4 * g) = float4{dc[0], dc[1], dc[2], dc[3]};
+  *reinterpret_cast<float4*>(D + i * SCAT_DLD + 16 + 4 * g) = float4{dc[4], dc[5], dc[6], dc[7]};
   {
     const int yb = g & 1, zb = g >> 1;
     const float wy = yb ? c.wy[1] : c.wy[0];
     const float wz = zb ? c.wz[1] : c.wz[0];
-    Wt[i * 8 + 2 * g] = (c.wx[0] * wy) * wz;
-    Wt[i * 8 + 2 * g + 1] = (c.wx[1] * wy) * wz;
+    Wt[(2 * g) * SCAT_KLD + i] = (c.wx[0] * wy) * wz;
+    Wt[(2 * g + 1) * SCAT_KLD + i] = (c.wx[1] * wy) * wz;
     if (G.grad_rows) {  // sparse gradient rows: the rows the forward claimed (-1: none, skipped)
       const int64_t v = ((c.z0 + zb) * G.dims[1] + (c.y0 + yb)) * G.dims[2] + c.x0;
       const int k0 = 2 * g, k1 = 2 * g + 1;
       const int r0 = ((c.inb >> k0) & 1u) ? G.grad_rows[v] : -1;
       const int r1 = ((c.inb >> k1) & 1u) ? G.grad_rows[v + 1] : -1;
-      OFF[i * 8 + k0] = r0 < 0 ? -1 : (int64_t)r0 * 32;
-      OFF[i * 8 + k1] = r1 < 0 ? -1 : (int64_t)r1 * 32;
+      OFF[k0 * SCAT_KLD + i] = r0 < 0 ? -1 : (int64_t)r0 * 32;
+      OFF[k1 * SCAT_KLD + i] = r1 < 0 ? -1 : (int64_t)r1 * 32;
     } else {
       const int64_t base = (c.z0 + zb) * G.grad_stride[1] + (c.y0 + yb) * G.grad_stride[2] + c.x0 * G.grad_stride[3];
-      OFF[i * 8 + 2 * g] = base;
-      OFF[i * 8 + 2 * g + 1] = base + G.grad_stride[3];
+      OFF[(2 * g) * SCAT_KLD + i] = base;
+      OFF[(2 * g + 1) * SCAT_KLD + i] = base + G.grad_stride[3];
     }
   }
   if (g == 0) {
     KEY[i] = valid ? (c.x0 | (c.y0 << 21) | (c.z0 << 42)) : -1;
     INB[i] = valid ? (int)c.inb : 0;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// (2) the walk over the staged 16 samples and the float atomics, by any one wave
+// (the staging wave itself, or a scatter wave of the workgroup: k_mlp_dx)
+__device__ __forceinline__ void grid_scatter_flush(const nc_grid& G, const float* reg, int lane) {
+  const float* D = reg;
+  const float* Wt = reg + SCAT_WT;
+  const int64_t* OFF = reinterpret_cast<const int64_t*>(reg + SCAT_OFF);
+  const int64_t* KEY = reinterpret_cast<const int64_t*>(reg + SCAT_KEY);
+  const int* INB = reinterpret_cast<const int*>(reg + SCAT_INB);
   const int half = lane >> 5, ch = lane & 31;
   const int64_t chs = G.grad_rows ? (int64_t)ch : (int64_t)ch * G.grad_stride[0];
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   auto flush = [&](int pt, int xb, int q, float v) {
     const int k = xb | (q << 1);
-    const int64_t o = OFF[pt * 8 + k];
+    const int64_t o = OFF[k * SCAT_KLD + pt];
     if (((INB[pt] >> k) & 1) && o >= 0) atomicAdd(G.grad + o + chs, v);
   };
   int run = 0;
@@ -150,13 +172,22 @@ __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c,
       }
       cur = kk;
     }
-    const float dv = D[pt * 32 + ch];
+    const float dv = D[pt * SCAT_DLD + ch];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = acc[q] + Wt[pt * 8 + half + 2 * q] * dv;
+    for (int q = 0; q < 4; ++q) acc[q] = acc[q] + Wt[(half + 2 * q) * SCAT_KLD + pt] * dv;
     run = pt;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) flush(run, half, q, acc[q]);
+}
+
+__device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c, const float dc[8], bool valid,
+                                             float* reg, int i, int g, int lane) {
+  grid_scatter_stage(G, c, dc, valid, reg, i, g);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  grid_scatter_flush(G, reg, lane);
 }
 
 

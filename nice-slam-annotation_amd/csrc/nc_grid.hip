@@ -103,6 +103,23 @@ __global__ void __launch_bounds__(256) k_grid_gather(const MlpCtx ctx) {
   *reinterpret_cast<float4*>(ctx.cfeat + job.c_off + p * job.c_stride + 4 * q) = o;
   if (ctx.claim_rows && q < 8 && G.grad_rows)  // sparse gradient rows: lane q claims corner q
     claim_row(G, co, q);
+  if (ctx.jac && q < 8) {  // NC_SAVE_POINT_JACOBIAN: d features / d (ix, iy, iz) of these 4 channels
+    float4 j[3] = {float4{0.f, 0.f, 0.f, 0.f}, float4{0.f, 0.f, 0.f, 0.f}, float4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int xb = k & 1, yb = (k >> 1) & 1, zb = k >> 2;
+      const bool in = (co.inb >> k) & 1u;
+      const float sx = in ? (xb ? 1.f : -1.f) * co.wy[yb] * co.wz[zb] : 0.f;
+      const float sy = in ? (yb ? 1.f : -1.f) * co.wx[xb] * co.wz[zb] : 0.f;
+      const float sz = in ? (zb ? 1.f : -1.f) * co.wx[xb] * co.wy[yb] : 0.f;
+      j[0].x = j[0].x + sx * v[k].x; j[0].y = j[0].y + sx * v[k].y; j[0].z = j[0].z + sx * v[k].z; j[0].w = j[0].w + sx * v[k].w;
+      j[1].x = j[1].x + sy * v[k].x; j[1].y = j[1].y + sy * v[k].y; j[1].z = j[1].z + sy * v[k].z; j[1].w = j[1].w + sy * v[k].w;
+      j[2].x = j[2].x + sz * v[k].x; j[2].y = j[2].y + sz * v[k].y; j[2].z = j[2].z + sz * v[k].z; j[2].w = j[2].w + sz * v[k].w;
+    }
+    float* dst = ctx.jac + ((int64_t)job.slot * ctx.P + p) * 96 + 4 * q;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) *reinterpret_cast<float4*>(dst + 32 * a) = j[a];
+  }
   if (ctx.share_mid && y == 1)  // the fine decoder's no-grad grid_middle lookup is this one
     *reinterpret_cast<float4*>(ctx.cfeat + ctx.jobs[0].c_off + p * ctx.jobs[0].c_stride + 32 + 4 * q) = o;
   if (ctx.zero_fill) {

@@ -53,6 +53,8 @@ struct MlpCtx {
                                   // (both split in proportion to the decoders' per-point MACs)
   float4* zero_fill;         // optional: k_grid_gather also zero-fills zero_n4 float4s here (the
   int64_t zero_n4;           // caller's gradient buffer, nc_render_args.grad_zero)
+  float* jac;                // NC_SAVE_POINT_JACOBIAN: [n_jobs][P][3][32] d own-grid features /
+                             // d (ix, iy, iz) (k_grid_gather -> k_mlp_dx), else NULL
   int32_t claim_rows;        // forward for a backward: k_grid_gather claims sparse gradient rows
                              // (nc_grid.grad_rows) of the grids that have a row map
   float* dfeat;              // NC_DETERMINISTIC: [n_jobs][P][32] d features of each job's own grid

@@ -535,18 +535,18 @@ static_assert(DX_SLICE_BASE % 4 == 0, "scatter slices are float4-aligned");
 constexpr int DX_LDS_FLOATS = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
 static_assert(DX_LDS_FLOATS * 4 <= 160 * 1024, "dX LDS budget");
 
-template <int KIND>
+template <int KIND, bool JAC>
 __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float* lds) {
   using N = Net<KIND>;
   using RC = Rec<KIND>;
-  load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int waves = blockDim.x >> 6;
   const bool need_dw = job.need_dw != 0;
   const bool need_grid = job.need_grid != 0;
   const bool need_coord = job.need_coord != 0;
   const bool need_dc = need_grid || need_coord;
+  load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
+  float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int64_t ntiles = (ctx.P + 15) / 16;
   for (int64_t t = (int64_t)blockIdx.x * waves + wave; t < ntiles; t += (int64_t)gridDim.x * waves) {
     asm volatile("" ::: "memory");  // keep LDS weight reads inside the loop (see fwd_job)
@@ -660,9 +660,21 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
 #else
       if (false) {
 #endif
-        float gi[3];
-        if (grid_vec_ok(G)) grid_coord_grad<true>(G, co, dcv, g, gi);
-        else grid_coord_grad<false>(G, co, dcv, g, gi);
+        float gi[3] = {0.f, 0.f, 0.f};
+        if (JAC) {  // the forward's trilinear Jacobian (NC_SAVE_POINT_JACOBIAN): no corner re-reads
+          const float* J = ctx.jac + ((int64_t)job.slot * ctx.P + (valid ? p : 0)) * 96 + 4 * g;
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            const float4 lo = *reinterpret_cast<const float4*>(J + 32 * a);
+            const float4 hi = *reinterpret_cast<const float4*>(J + 32 * a + 16);
+            gi[a] = lo.x * dcv[0] + lo.y * dcv[1] + lo.z * dcv[2] + lo.w * dcv[3] +
+                    hi.x * dcv[4] + hi.y * dcv[5] + hi.z * dcv[6] + hi.w * dcv[7];
+          }
+        } else if (grid_vec_ok(G)) {
+          grid_coord_grad<true>(G, co, dcv, g, gi);
+        } else {
+          grid_coord_grad<false>(G, co, dcv, g, gi);
+        }
         const float gm[3] = {co.gmx, co.gmy, co.gmz};
         const nc_decoder_params& D = ctx.dec[KIND];
 #pragma unroll
@@ -694,15 +706,18 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
   }
 }
 
+// JAC: the coordinate gradient from the forward's saved Jacobian (NC_SAVE_POINT_JACOBIAN);
+// its own instantiation, so the corner re-read path's registers do not weigh on it
+template <bool JAC>
 __global__ void __launch_bounds__(DX_THREADS) k_mlp_dx(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Job job = pick_job(ctx.jobs, blockIdx.y);
   if (!job.need_dw && !job.need_grid && !job.need_coord) return;
   switch (job.kind) {
-    case K_COARSE: dx_job<K_COARSE>(ctx, job, lds); break;
-    case K_MID: dx_job<K_MID>(ctx, job, lds); break;
-    case K_FINE: dx_job<K_FINE>(ctx, job, lds); break;
-    default: dx_job<K_COLOR>(ctx, job, lds); break;
+    case K_COARSE: dx_job<K_COARSE, JAC>(ctx, job, lds); break;
+    case K_MID: dx_job<K_MID, JAC>(ctx, job, lds); break;
+    case K_FINE: dx_job<K_FINE, JAC>(ctx, job, lds); break;
+    default: dx_job<K_COLOR, JAC>(ctx, job, lds); break;
   }
 }
 
@@ -1037,8 +1052,9 @@ int mlp_blocks_per_cu(int which) {
       set_lds(k_mlp_fwd, mlp_fwd_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd, FWD_THREADS, mlp_fwd_lds_bytes());
     } else if (which == 1) {
-      set_lds(k_mlp_dx, mlp_dx_lds_bytes());
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dx, DX_THREADS, mlp_dx_lds_bytes());
+      set_lds(k_mlp_dx<true>, mlp_dx_lds_bytes());
+      set_lds(k_mlp_dx<false>, mlp_dx_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dx<true>, DX_THREADS, mlp_dx_lds_bytes());
     } else {
       set_lds(k_mlp_dw, mlp_dw_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dw, DW_THREADS, mlp_dw_lds_bytes());
@@ -1068,8 +1084,12 @@ int mlp_dx_lds_bytes() { return DX_LDS_FLOATS * 4; }
 
 int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s) {
   static int attr = -1;
-  if (attr != 0 && (attr = set_lds(k_mlp_dx, mlp_dx_lds_bytes())) != 0) return attr;
-  hipLaunchKernelGGL(k_mlp_dx, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
+  if (attr != 0 && (attr = set_lds(k_mlp_dx<true>, mlp_dx_lds_bytes()) | set_lds(k_mlp_dx<false>, mlp_dx_lds_bytes())) != 0)
+    return attr;
+  if (c.jac)
+    hipLaunchKernelGGL(k_mlp_dx<true>, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
+  else
+    hipLaunchKernelGGL(k_mlp_dx<false>, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "libnicecore.so")
 NC_ABI_VERSION = 5
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
+NC_SAVE_POINT_JACOBIAN = 4
 NC_LOSS_NONE, NC_LOSS_MAPPER, NC_LOSS_TRACKER = 0, 1, 2
 NC_LOSS_COLOR, NC_LOSS_DYNAMIC = 1, 2
 NC_MAX_SAMPLES = 64

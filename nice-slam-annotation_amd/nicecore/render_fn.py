@@ -62,12 +62,20 @@ def deterministic_requested(spec=None) -> bool:
 # the forward zero-fills the backward's grid-gradient buffer (nc_render_args.grad_zero);
 # NICECORE_FWD_ZERO=0 falls back to a separate fill in the backward (A/B timing)
 _FWD_ZERO = os.environ.get("NICECORE_FWD_ZERO", "1") != "0"
+# the forward keeps the trilinear Jacobian for the coordinate gradient (NC_SAVE_POINT_JACOBIAN);
+# NICECORE_SAVE_JAC=0 makes the backward re-read the grid corners instead (A/B, tests)
+_SAVE_JAC = os.environ.get("NICECORE_SAVE_JAC", "1") != "0"
 
 
-def _flags(ctx, spec):
+def _flags(ctx, spec, coord_inputs=()):
+    """NC_SAVE_FOR_BACKWARD when anything needs a gradient; NC_SAVE_POINT_JACOBIAN when
+    the inputs at ``coord_inputs`` (rays / points) do; NC_DETERMINISTIC on request."""
     if not any(ctx.needs_input_grad):
         return 0
-    return L.NC_SAVE_FOR_BACKWARD | (L.NC_DETERMINISTIC if deterministic_requested(spec) else 0)
+    f = L.NC_SAVE_FOR_BACKWARD | (L.NC_DETERMINISTIC if deterministic_requested(spec) else 0)
+    if _SAVE_JAC and any(ctx.needs_input_grad[i] for i in coord_inputs):
+        f |= L.NC_SAVE_POINT_JACOBIAN
+    return f
 
 
 def decoder_modules(decoders):
@@ -381,7 +389,7 @@ class NiceRenderFn(torch.autograd.Function):
         N = rays_o.shape[0]
         a = L.NcRenderArgs.from_buffer_copy(
             plan.render_template(device, spec["n_strat"], spec["n_surf"], spec["bound"]))
-        a.flags = _flags(ctx, spec)
+        a.flags = _flags(ctx, spec, (1, 2))
         a.n_rays = N
         a.rays_o = rays_o.data_ptr()
         a.rays_d = rays_d.data_ptr()
@@ -488,7 +496,7 @@ class NiceEvalFn(torch.autograd.Function):
         P = pts.shape[0]
         a = L.NcPointsArgs.from_buffer_copy(plan.points_template(device))
         a.n_points = P
-        a.flags = _flags(ctx, spec)
+        a.flags = _flags(ctx, spec, (1,))
         a.pts = pts.data_ptr()
         grids = (g0, g1, g2, g3)
         gkeep = []
