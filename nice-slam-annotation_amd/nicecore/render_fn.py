@@ -62,9 +62,12 @@ def deterministic_requested(spec=None) -> bool:
 # the forward zero-fills the backward's grid-gradient buffer (nc_render_args.grad_zero);
 # NICECORE_FWD_ZERO=0 falls back to a separate fill in the backward (A/B timing)
 _FWD_ZERO = os.environ.get("NICECORE_FWD_ZERO", "1") != "0"
-# the forward keeps the trilinear Jacobian for the coordinate gradient (NC_SAVE_POINT_JACOBIAN);
-# NICECORE_SAVE_JAC=0 makes the backward re-read the grid corners instead (A/B, tests)
-_SAVE_JAC = os.environ.get("NICECORE_SAVE_JAC", "1") != "0"
+# NICECORE_SAVE_JAC=1: the forward keeps the trilinear Jacobian for the coordinate gradient
+# (NC_SAVE_POINT_JACOBIAN) instead of the backward re-reading the grid corners.  Off by
+# default: measured at C2 it moves as much time into k_grid_gather (+6..12 us, 55 MB more
+# writes) as it saves in k_mlp_dx (-6..7 us) -- BA 0.393 vs 0.399 ms, tracker 0.2065 vs
+# 0.2076 ms per step (profiles/r01/jacobian_ab.txt)
+_SAVE_JAC = os.environ.get("NICECORE_SAVE_JAC", "0") == "1"
 
 
 def _flags(ctx, spec, coord_inputs=()):
