@@ -37,13 +37,13 @@ enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
   KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
-  KID_ROWS_MERGE, KID_COUNT
+  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
-                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge"};
+                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -164,6 +164,9 @@ struct Ws {
   bool det = false;
   size_t jac = 0;
   bool has_jac = false;
+  size_t claim_cnt = 0, claim_tmp = 0;  // sparse-row claims (nc_grid.grad_rows)
+  int64_t claim_cap = 0;
+  bool claims = false;
   int vbits = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
@@ -192,7 +195,7 @@ void split_wgs(int total, int64_t blocks, const Job* jobs, int n_jobs, int32_t* 
 }
 
 void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1,
-            bool jac = false) {
+            bool jac = false, bool claims = false) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -211,6 +214,13 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
   w.dpts = take((size_t)pl.n_jobs * P * 24);
   w.jac = (save && jac) ? take((size_t)pl.n_jobs * P * 96 * 4) : 0;
   w.has_jac = save && jac;
+  w.claims = save && claims;
+  if (w.claims) {  // per-shard claim lists of k_grid_gather: every lane of a shard's waves fits
+    const int64_t waves = (P * 16 + 255) / 256 * 4;  // gather waves of the widest job
+    w.claim_cap = ((waves + CLAIM_SHARDS - 1) / CLAIM_SHARDS + 1) * 64;
+    w.claim_cnt = take((size_t)MAX_JOBS * CLAIM_SHARDS * 4);
+    w.claim_tmp = take((size_t)MAX_JOBS * CLAIM_SHARDS * w.claim_cap * 8);
+  }
   if (loss) {  // per-ray loss derivatives, forward -> backward
     w.coef_d = take((size_t)N * 8);
     w.coef_c = take((size_t)N * 12);
@@ -302,7 +312,12 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.slab = at<float>(ws, w.slab);
   m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
   m.cfeat = w.save ? m.rec : at<float>(ws, w.feat);
-  m.claim_rows = w.save;  // only grids with a row map (nc_grid.grad_rows) claim
+  m.claim_rows = w.claims;  // only grids with a row map (nc_grid.grad_rows) claim
+  if (w.claims) {
+    m.claim_cnt = at<int32_t>(ws, w.claim_cnt);
+    m.claim_tmp = at<int64_t>(ws, w.claim_tmp);
+    m.claim_cap = w.claim_cap;
+  }
   m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
   m.jac = w.has_jac ? at<float>(ws, w.jac) : nullptr;
 }
@@ -331,6 +346,26 @@ int stage_vbits(const Plan& pl, const nc_grid* grids) {
   int b = 1;
   while ((uint64_t(1) << b) < most) ++b;
   return b;
+}
+
+// sparse gradient rows: does any decoder of the stage claim rows of its own grid?
+bool stage_claims(const Plan& pl, const nc_grid* grids) {
+  for (int j = 0; j < pl.n_jobs; ++j)
+    if (grids[pl.jobs[j].kind].grad_rows) return true;
+  return false;
+}
+
+// k_grid_gather with sparse-row claims: zero the shard counters, gather (claims),
+// give the claims their rows (k_rows_compact)
+int gather_and_claim(MlpCtx& m, const Ws& w, hipStream_t s) {
+  if (w.claims)
+    if (int e = check_hip(hipMemsetAsync(m.claim_cnt, 0, (size_t)MAX_JOBS * CLAIM_SHARDS * 4, s), "claim counters"))
+      return e;
+  if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
+  if (w.claims)
+    if (int e = check_hip(timed(KID_ROWS_CLAIM, s, [&] { return launch_rows_compact(m, s); }), "k_rows_compact"))
+      return e;
+  return 0;
 }
 
 int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S) {
@@ -363,7 +398,7 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
   layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w, vbits,
-         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0);
+         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids));
   if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }
@@ -568,7 +603,7 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     m.zero_fill = reinterpret_cast<float4*>(a->grad_zero);
     m.zero_n4 = a->grad_zero_floats / 4;
   }
-  if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
+  if (int e = gather_and_claim(m, w, s)) return e;
   m.zero_fill = nullptr;
   m.zero_n4 = 0;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
@@ -617,7 +652,7 @@ static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
   layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w, vbits,
-         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0);
+         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids));
   if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }
@@ -641,7 +676,7 @@ int nc_points_forward(const nc_points_args* a, void* ws, size_t ws_bytes, void* 
   MlpCtx m;
   fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, false);
   if (int e = check_hip(launch_points_prep(m, (float4*)m.xyz, (float4*)m.pf, s), "k_points_prep")) return e;
-  if (int e = check_hip(timed(KID_GRID_GATHER, s, [&] { return launch_grid_gather(m, s); }), "k_grid_gather")) return e;
+  if (int e = gather_and_claim(m, w, s)) return e;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
   return check_hip(timed(KID_POINTS_ASSEMBLE, s, [&] { return launch_points_assemble(m, a->stage, a->raw, s); }), "k_points_assemble");
 }

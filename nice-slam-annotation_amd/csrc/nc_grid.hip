@@ -10,12 +10,12 @@ __device__ __forceinline__ Job pick_job3(const Job (&jobs)[MAX_JOBS], unsigned y
 }
 
 // Sparse gradient rows (nc_grid.grad_rows, ABI v5): the first lookup that touches an
-// in-bounds voxel claims it a gradient row -- compare-and-swap -1 -> -2 on the map
-// entry, then one counter atomic per wavefront for all of its winners -- zero-fills
-// the row and records the voxel.  The backward (nc_grid.h grid_scatter) accumulates
-// into rows[voxel].  An overflowing claim (row >= capacity) is undone (map back to
-// -1; the counter keeps the overshoot, which the caller checks).
-__device__ __forceinline__ void claim_row(const nc_grid& G, const Corners& co, int k) {
+// in-bounds voxel claims it -- compare-and-swap -1 -> -2 on the map entry -- and
+// appends the voxel to its wavefront's shard list (one counter atomic per wavefront,
+// spread over CLAIM_SHARDS counters).  k_rows_compact (nc_sparse.hip) then gives the
+// claims contiguous rows after the existing ones, points the map at them and zeroes
+// them.  The backward (nc_grid.h grid_scatter) accumulates into rows[voxel].
+__device__ __forceinline__ void claim_row(const MlpCtx& ctx, const nc_grid& G, const Corners& co, int k) {
   const bool in = (co.inb >> k) & 1u;
   const int64_t x = co.x0 + (k & 1), y = co.y0 + ((k >> 1) & 1), z = co.z0 + (k >> 2);
   const int64_t v = in ? (z * G.dims[1] + y) * G.dims[2] + x : 0;
@@ -26,20 +26,15 @@ __device__ __forceinline__ void claim_row(const nc_grid& G, const Corners& co, i
   if (m == 0) return;
   const int leader = __builtin_ctzll(m);
   const int lane = __lane_id();
+  const int shard = (int)(((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % CLAIM_SHARDS);
+  int32_t* cnt = ctx.claim_cnt + blockIdx.y * CLAIM_SHARDS + shard;
   int base = 0;
-  if (lane == leader) base = atomicAdd(G.row_count, (int)__builtin_popcountll(m));
+  if (lane == leader) base = atomicAdd(cnt, (int)__builtin_popcountll(m));
   base = __shfl(base, leader);
   if (!won) return;
-  const int64_t row = base + (int64_t)__builtin_popcountll(m & ((uint64_t(1) << lane) - 1));
-  if (row >= G.row_capacity) {
-    atomicExch(G.grad_rows + v, -1);
-    return;
-  }
-  G.row_voxel[row] = v;
-  float4* dst = reinterpret_cast<float4*>(G.grad + row * 32);
-#pragma unroll
-  for (int c = 0; c < 8; ++c) dst[c] = float4{0.f, 0.f, 0.f, 0.f};
-  atomicExch(G.grad_rows + v, (int)row);
+  const int64_t slot = base + (int64_t)__builtin_popcountll(m & ((uint64_t(1) << lane) - 1));
+  if (slot < ctx.claim_cap)  // (by construction: claim_cap covers every lane of the shard's waves)
+    ctx.claim_tmp[((int64_t)blockIdx.y * CLAIM_SHARDS + shard) * ctx.claim_cap + slot] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -102,7 +97,7 @@ __global__ void __launch_bounds__(256) k_grid_gather(const MlpCtx ctx) {
   }
   *reinterpret_cast<float4*>(ctx.cfeat + job.c_off + p * job.c_stride + 4 * q) = o;
   if (ctx.claim_rows && q < 8 && G.grad_rows)  // sparse gradient rows: lane q claims corner q
-    claim_row(G, co, q);
+    claim_row(ctx, G, co, q);
   if (ctx.jac && q < 8) {  // NC_SAVE_POINT_JACOBIAN: d features / d (ix, iy, iz) of these 4 channels
     float4 j[3] = {float4{0.f, 0.f, 0.f, 0.f}, float4{0.f, 0.f, 0.f, 0.f}, float4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll

@@ -45,6 +45,65 @@ int launch_rows_clear(const nc_sparse_rows& r, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// k_rows_compact: the forward's per-shard claim lists (k_grid_gather) -> rows
+// [count, count + claims) in shard order: row_voxel, the map entry, a zeroed row.
+// Grid (chunk, shard s, job y); thread = (claim, 4-channel chunk).  k_rows_commit then
+// advances the row counter (a claim past the capacity is undone: map -1; the counter
+// keeps the overshoot, which the caller checks).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ nc_grid claim_grid(const MlpCtx& m, int y) {
+  const int kind = y == 0 ? m.jobs[0].kind : (y == 1 ? m.jobs[1].kind : m.jobs[2].kind);
+  return kind == 0 ? m.grids[0] : kind == 1 ? m.grids[1] : kind == 2 ? m.grids[2] : m.grids[3];
+}
+
+__global__ void __launch_bounds__(256) k_rows_compact(const MlpCtx m) {
+  const int s = blockIdx.y, y = blockIdx.z;
+  const nc_grid G = claim_grid(m, y);
+  if (!G.grad_rows) return;
+  const int32_t* cnt = m.claim_cnt + y * CLAIM_SHARDS;
+  const int64_t n = min((int64_t)cnt[s], m.claim_cap);
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (claim, 4-channel chunk)
+  if (e >= n * 8) return;
+  int64_t prefix = 0;
+  for (int t = 0; t < s; ++t) prefix += min((int64_t)cnt[t], m.claim_cap);
+  const int64_t base = (int64_t)*G.row_count + prefix;
+  const int64_t* tmp = m.claim_tmp + ((int64_t)y * CLAIM_SHARDS + s) * m.claim_cap;
+  {
+    const int64_t l = e >> 3;
+    const int c = (int)(e & 7);
+    const int64_t v = tmp[l], r = base + l;
+    if (r < G.row_capacity) {
+      reinterpret_cast<float4*>(G.grad + r * 32)[c] = float4{0.f, 0.f, 0.f, 0.f};
+      if (c == 0) {
+        G.row_voxel[r] = v;
+        G.grad_rows[v] = (int32_t)r;
+      }
+    } else if (c == 0) {
+      G.grad_rows[v] = -1;
+    }
+  }
+}
+
+__global__ void k_rows_commit(const MlpCtx m) {
+  const int y = threadIdx.x;  // one thread per job
+  if (y >= m.n_jobs) return;
+  const nc_grid G = claim_grid(m, y);
+  if (!G.grad_rows) return;
+  int64_t total = 0;
+  for (int t = 0; t < CLAIM_SHARDS; ++t) total += min((int64_t)m.claim_cnt[y * CLAIM_SHARDS + t], m.claim_cap);
+  *G.row_count = (int32_t)min((int64_t)*G.row_count + total, (int64_t)INT32_MAX);
+}
+
+int launch_rows_compact(const MlpCtx& m, hipStream_t s) {
+  // one thread per (claim, chunk) of a full shard; blocks past a shard's count exit at once
+  const int64_t bx = (m.claim_cap * 8 + 255) / 256;
+  hipLaunchKernelGGL(k_rows_compact, dim3((unsigned)bx, CLAIM_SHARDS, m.n_jobs), dim3(256), 0, s, m);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  hipLaunchKernelGGL(k_rows_commit, dim3(1), dim3(64), 0, s, m);
+  return (int)hipGetLastError();
+}
+
 struct MergeBufs {
   uint64_t* key[2];  // [n] unsorted / sorted voxel keys
   int32_t* head;     // [n] 1 at the first key of a voxel
