@@ -213,23 +213,24 @@ FEAT = {"coarse": 32, "middle": 32, "fine": 64, "color": 32}
 NOUT = {"coarse": 1, "middle": 1, "fine": 1, "color": 3}
 
 
-def algorithmic_bytes_per_point(stage, mode):
+def algorithmic_bytes_per_point(stage, mode, jac=False):
     """HBM bytes a kernel must move per sample point: its inputs and
     outputs, the saved activation records included (they are the backward's input)."""
     decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
             "color": ["fine", "middle", "color"]}[stage]
     fwd = sum(4 * FEAT[d] + 16 + 4 * (REC_LEN[d] - FEAT[d]) + 4 * NOUT[d] for d in decs)
     # k_mlp_dx per decoder: masks 32 B + d out + p.float() 16 B + normalised xyz 16 B in,
-    # point gradient 24 B out, the saved trilinear Jacobian 384 B in (NC_SAVE_POINT_JACOBIAN);
-    # BA mode adds the backward record out and the grid-gradient scatter, counted as
-    # SURVEY.md §8(d) does: 2 x 1,024 B (read-modify-write of 8 corner rows) per lookup
+    # point gradient 24 B out, and for the coordinate gradient either the 8 corner rows
+    # re-gathered (1,024 B, SURVEY.md §8(d)) or the saved trilinear Jacobian (384 B,
+    # NC_SAVE_POINT_JACOBIAN); BA mode adds the backward record out and the grid-gradient
+    # scatter, counted as §8(d) does: 2 x 1,024 B (read-modify-write of 8 corner rows)
     ba = mode == "ba"
-    dx = sum(32 + 4 * NOUT[d] + 16 + 16 + 24 + 384 +
+    dx = sum(32 + 4 * NOUT[d] + 16 + 16 + 24 + (384 if jac else 1024) +
              ((4 * (REC_STRIDE[d] - REC_LEN[d]) + 2 * 1024) if ba else 0) for d in decs)
     dw = sum(4 * REC_STRIDE[d] for d in decs) if mode == "ba" else 0
     # k_grid_gather: 8 corner rows of 128 B per distinct lookup, 128 B of features out per
     # lookup, and the 384-B trilinear Jacobian of each decoder's own lookup (ray gradients)
-    gather = 1024 * LOOKUPS_UNIQUE[stage] + 128 * LOOKUPS_FWD[stage] + 384 * len(decs)
+    gather = 1024 * LOOKUPS_UNIQUE[stage] + 128 * LOOKUPS_FWD[stage] + (384 * len(decs) if jac else 0)
     return {"k_mlp_fwd": fwd, "k_mlp_dx": dx, "k_mlp_dw": dw, "k_grid_gather": gather}
 
 
@@ -361,7 +362,8 @@ def main():
 
     S = 32 if args.stage == "coarse" else 48  # the coarse mapper renders without gt depth (Mapper.py:600)
     per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode)
-    per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode)
+    from nicecore import render_fn as RF
+    per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode, jac=RF._SAVE_JAC)
     fl = per_ray[dominant] * args.rays if dominant in per_ray else None
     by = per_pt_bytes[dominant] * args.rays * S if dominant in per_pt_bytes else None
     roof = None
