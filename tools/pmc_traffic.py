@@ -18,9 +18,12 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
+        if name.startswith("void "):
+            name = name[5:]
         if not name.startswith("nc::"):
             continue
-        acc[name.split("(")[0].replace("nc::", "")].append(float(r["Counter_Value"]))
+        # "nc::k_mlp_dx<false>(nc::MlpCtx)" -> "k_mlp_dx"
+        acc[name.split("(")[0].split("<")[0].replace("nc::", "")].append(float(r["Counter_Value"]))
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
