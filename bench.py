@@ -142,6 +142,7 @@ def make_step(w, args, world, device):
     sparse = w["sparse"]
     gvals = [g for k, g in grids.items() if g.requires_grad and (sparse is None or k not in sparse.rows)]
     dmax = gt.max().reshape(1).clone() if world > 1 else None  # static buffer
+    one = torch.ones((), dtype=torch.float64, device=device)  # d loss / d loss, allocated once
     loss_kw = LOSS_KW[args.mode](args.stage)
 
     def pre():
@@ -159,7 +160,7 @@ def make_step(w, args, world, device):
         depth, unc, color, loss = renderer.render_batch_loss(
             grids, model, rd, ro, device, args.stage, gt, gtc, **loss_kw, depth_max=dmax,
             sparse_grads=sparse)
-        loss.backward()
+        loss.backward(one)  # = loss.backward(), without a fill kernel per step
         return loss
 
     def post():

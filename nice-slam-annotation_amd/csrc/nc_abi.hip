@@ -37,13 +37,13 @@ enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
   KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
-  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_COUNT
+  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
-                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact"};
+                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -472,11 +472,12 @@ int64_t nparam_of(int kind) {
   return -1;
 }
 
-int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s);
+int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s, const RayCtx* rc);
 
 // decoder backward: dX chains + trilinear backward (k_mlp_dx) -> weight gradients
 // -> slab reduction
-int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s, const DetBufs* det) {
+int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s, const DetBufs* det,
+                 const RayCtx* rc = nullptr) {
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
   if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs, 1), s); }), "k_mlp_dx")) return e;
   bool any_grid = false;
@@ -487,10 +488,11 @@ int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipSt
   for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;
   if (any_dw)
     if (int e = check_hip(timed(KID_MLP_DW, s, [&] { return launch_mlp_dw(m, s); }), "k_mlp_dw")) return e;
-  return reduce_params(m, dec, s);
+  return reduce_params(m, dec, s, rc);
 }
 
-int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s) {
+// slab reduction of the weight gradients; with rc, d rays_o / d rays_d in the same launch
+int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s, const RayCtx* rc) {
   ParamReduceCtx r;
   std::memset(&r, 0, sizeof(r));
   r.n_jobs = m.n_jobs;
@@ -505,7 +507,13 @@ int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s) 
     r.nparam[j] = nparam_of(m.jobs[j].kind);
     any |= (r.grad[j] != nullptr);
   }
-  if (!any) return 0;
+  if (!any) {
+    if (!rc) return 0;
+    return check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(*rc, s); }), "k_ray_grads");
+  }
+  if (rc)
+    return check_hip(timed(KID_PARAM_RAY, s, [&] { return launch_param_ray_reduce(r, max_param_count(), *rc, s); }),
+                     "k_param_ray_reduce");
   return check_hip(timed(KID_PARAM_REDUCE, s, [&] { return launch_param_reduce(r, max_param_count(), s); }), "k_param_reduce");
 }
 
@@ -633,10 +641,7 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   if (!any) return 0;
   if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
   const DetBufs det = det_bufs(ws, w);
-  if (int e = mlp_backward(m, a->dec, P, s, &det)) return e;
-  if (need_coord)
-    if (int e = check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(rc, s); }), "k_ray_grads")) return e;
-  return 0;
+  return mlp_backward(m, a->dec, P, s, &det, need_coord ? &rc : nullptr);  // (+ ray grads, fused)
 }
 
 static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {

@@ -163,6 +163,7 @@ int launch_composite_bwd(const RayCtx& c, hipStream_t s);
 int launch_ray_grads(const RayCtx& c, hipStream_t s);
 int launch_loss(const RayCtx& c, hipStream_t s);
 int launch_param_reduce(const ParamReduceCtx& c, int64_t max_nparam, hipStream_t s);
+int launch_param_ray_reduce(const ParamReduceCtx& c, int64_t max_nparam, const RayCtx& rc, hipStream_t s);
 int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s);
 int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, float* gocc, float* grgb,
                              hipStream_t s);

@@ -435,9 +435,9 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_ray_grads(const RayCtx c) {
+__device__ __forceinline__ void ray_grads_body(const RayCtx& c, int64_t block) {
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  const int64_t r = block * RAY_WAVES + (threadIdx.x >> 6);
   if (r >= c.N) return;
   const bool act = lane < c.S;
   const int64_t p = r * c.S + (act ? lane : 0);
@@ -460,20 +460,22 @@ __global__ void __launch_bounds__(256) k_ray_grads(const RayCtx c) {
   }
 }
 
+__global__ void __launch_bounds__(256) k_ray_grads(const RayCtx c) { ray_grads_body(c, blockIdx.x); }
+
 // thread = (float4 column of the parameter vector, part): part p sums slab rows
 // p, p+8, ... (independent loads in flight), the 8 partial sums meet in LDS.
 constexpr int PR_COLS = 32, PR_PARTS = 8;
-__global__ void __launch_bounds__(PR_COLS * PR_PARTS) k_param_reduce(const ParamReduceCtx c) {
+static_assert(PR_COLS * PR_PARTS == 64 * RAY_WAVES, "k_param_ray_reduce: one block size for both roles");
+__device__ __forceinline__ void param_reduce_body(const ParamReduceCtx& c, int bx, int j) {
   __shared__ float4 part[PR_PARTS][PR_COLS];
-  const int j = blockIdx.y;
   // constant-index selects (dynamic indexing of the argument block spills it)
   const Job job = j == 0 ? c.jobs[0] : (j == 1 ? c.jobs[1] : c.jobs[2]);
   float* grad = j == 0 ? c.grad[0] : (j == 1 ? c.grad[1] : c.grad[2]);
   const int64_t np = j == 0 ? c.nparam[0] : (j == 1 ? c.nparam[1] : c.nparam[2]);
   if (!job.need_dw || grad == nullptr) return;
   const int col = threadIdx.x % PR_COLS, prt = threadIdx.x / PR_COLS;
-  const int64_t e = ((int64_t)blockIdx.x * PR_COLS + col) * 4;  // first parameter of the column
-  if ((int64_t)blockIdx.x * PR_COLS * 4 >= np) return;          // whole workgroup past the end
+  const int64_t e = ((int64_t)bx * PR_COLS + col) * 4;  // first parameter of the column
+  if ((int64_t)bx * PR_COLS * 4 >= np) return;          // whole workgroup past the end
   float4 acc = float4{0.f, 0.f, 0.f, 0.f};
   if (e < c.slab_stride) {  // slab rows are padded to slab_stride (multiple of 64 floats)
     const int w0 = j == 0 ? c.wg_off[0] : (j == 1 ? c.wg_off[1] : c.wg_off[2]);
@@ -498,6 +500,19 @@ __global__ void __launch_bounds__(PR_COLS * PR_PARTS) k_param_reduce(const Param
     for (int k = 0; k < 4; ++k)
       if (e + k < np) grad[e + k] = sv[k];
   }
+}
+
+__global__ void __launch_bounds__(PR_COLS * PR_PARTS) k_param_reduce(const ParamReduceCtx c) {
+  param_reduce_body(c, blockIdx.x, blockIdx.y);
+}
+
+// the backward's last two steps in one launch: blocks [0, pr_blocks) sum the weight-
+// gradient slabs (job = b / pr_x), the rest form d rays_o / d rays_d
+__global__ void __launch_bounds__(PR_COLS * PR_PARTS) k_param_ray_reduce(const ParamReduceCtx pc, const RayCtx rc,
+                                                                        int pr_x, int pr_blocks) {
+  const int b = blockIdx.x;
+  if (b < pr_blocks) param_reduce_body(pc, b % pr_x, b / pr_x);
+  else ray_grads_body(rc, b - pr_blocks);
 }
 
 // ---- NICE.forward on caller points (decoder.py:336-370) ----
@@ -567,6 +582,13 @@ int launch_ray_grads(const RayCtx& c, hipStream_t s) {
 int launch_param_reduce(const ParamReduceCtx& c, int64_t max_nparam, hipStream_t s) {
   dim3 grid((unsigned)((max_nparam + 4 * PR_COLS - 1) / (4 * PR_COLS)), c.n_jobs);
   hipLaunchKernelGGL(k_param_reduce, grid, dim3(PR_COLS * PR_PARTS), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_param_ray_reduce(const ParamReduceCtx& c, int64_t max_nparam, const RayCtx& rc, hipStream_t s) {
+  const int pr_x = (int)((max_nparam + 4 * PR_COLS - 1) / (4 * PR_COLS));
+  const int pr_blocks = pr_x * c.n_jobs;
+  hipLaunchKernelGGL(k_param_ray_reduce, dim3((unsigned)(pr_blocks + ray_blocks(rc.N))), dim3(PR_COLS * PR_PARTS), 0,
+                     s, c, rc, pr_x, pr_blocks);
   return (int)hipGetLastError();
 }
 int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s) {

@@ -157,7 +157,8 @@ KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_f
               "k_points_assemble": 8, "k_points_split_grad": 9, "k_points_grads": 10,
               "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15,
               "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18,
-              "k_rows_clear": 19, "k_rows_merge": 20, "k_rows_compact": 21}
+              "k_rows_clear": 19, "k_rows_merge": 20, "k_rows_compact": 21,
+              "k_param_ray_reduce": 22}
 
 
 class KernelTimer:
