@@ -99,8 +99,8 @@ def test_fused_loss_matches_oracle(case, kind, color_term, dyn):
 @pytest.mark.parametrize("kind,color_term,dyn", [("tracker", True, True), ("mapper", True, False)])
 def test_fused_loss_room0_sizes(n_rays, kind, color_term, dyn):
     """Replica room0 scene at the mapper's / tracker's batch sizes and beyond one ray
-    per thread of k_loss: the median by rank counting (N <= 1024) and by radix select
-    (1025, 4099 > 4 x 1024), strided sums."""
+    per thread of k_loss (1024, 1025, 4099 > 4 x 1024): median radix select, strided
+    sums."""
     from test_gpu_parity import _room0_case
     sc, grids, params, ro, rd, dep = _room0_case(n_rays, "color", seed=11)
     model = build_model(params, sc.bound, sc.bound * 2, "cuda")
