@@ -245,3 +245,48 @@ def test_sparse_allreduce_two_gloo_ranks(tmp_path):
         dense[outs[0][k + "/idx"]] = outs[0][k + "/val"]
         dense = dense.reshape(1, D, H, W, 32).permute(0, 4, 1, 2, 3)
         assert rel_err(dense, ref[k]) <= 1e-5, k
+
+
+@pytest.mark.gpu
+def test_sparse_rows_drive_sparse_adam():
+    """coo() is the gradient of the channels-last row view: a torch.optim.SparseAdam step
+    with it equals the SparseAdam step with the dense path's gradient made sparse
+    (SparseAdam's eps enters after the bias correction, unlike dense Adam's, so the
+    comparison is sparse-with-sparse)."""
+    from nicecore.sparse import SparseGridGrads
+    sc, g, model, ro, rd, dep = _setup(300, seed=71)
+    # ordered reductions: the sparse and dense gradients are bit-identical, so entries
+    # whose contributions cancel cannot flip sign between the two
+    _run(sc, g, model, ro, rd, dep, deterministic=True)
+    dense = g["grid_fine"].grad.detach().permute(0, 2, 3, 4, 1).reshape(-1, 32).clone()
+    _clear(g, model)
+    sp = SparseGridGrads(g, keys=("grid_fine",))
+    _run(sc, g, model, ro, rd, dep, sparse=sp, deterministic=True)
+    grid = g["grid_fine"]
+    rows = grid.detach().permute(0, 2, 3, 4, 1).reshape(-1, 32)  # a view of the channels-last grid
+    assert rows.data_ptr() == grid.data_ptr()
+    ps = torch.nn.Parameter(rows.clone())
+    ps.grad = sp.coo("grid_fine")
+    torch.optim.SparseAdam([ps], lr=1e-2).step()
+    pd = torch.nn.Parameter(rows.clone())
+    pd.grad = dense.to_sparse(sparse_dim=1)
+    torch.optim.SparseAdam([pd], lr=1e-2).step()
+    assert torch.allclose(ps.detach(), pd.detach(), rtol=0, atol=1e-7)
+    assert not torch.equal(ps.detach(), rows)
+
+
+@pytest.mark.gpu
+def test_sparse_rows_overflow_is_reported():
+    """A capacity smaller than the claims (rows fixed by hand, no growth) is reported,
+    not silently truncated."""
+    from nicecore import _lib as L
+    from nicecore.sparse import SparseGridGrads
+    sc, g, model, ro, rd, dep = _setup(200, seed=73)
+    sp = SparseGridGrads(g, keys=("grid_fine",), capacity=16)
+    r = sp.rows["grid_fine"]
+    r.reserve = lambda extra: None  # keep the 16 rows
+    _run(sc, g, model, ro, rd, dep, sparse=sp)
+    with pytest.raises(L.NiceCoreError, match="overflowed"):
+        sp.count("grid_fine")
+    sp.zero_grad()
+    assert bool((r.map == -1).all())
