@@ -25,6 +25,7 @@ constexpr int MAX_JOBS = 3;
 // sparse-row claims: wavefront w of a job appends to counter w % CLAIM_SHARDS (one hot
 // word saturates near 88 returning atomics per microsecond, MI355X_MICROARCH.md)
 constexpr int CLAIM_SHARDS = 64;
+static_assert(CLAIM_SHARDS <= 64, "k_rows_compact sums the shard counters across one wavefront");
 
 // Arguments of the point-batched decoder kernels.
 struct MlpCtx {

@@ -48,7 +48,7 @@ int launch_rows_clear(const nc_sparse_rows& r, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // k_rows_compact: the forward's per-shard claim lists (k_grid_gather) -> rows
 // [count, count + claims) in shard order: row_voxel, the map entry, a zeroed row.
-// Grid (chunk, shard s, job y); thread = (claim, 4-channel chunk).  k_rows_commit then
+// Grid (up to 16 blocks, shard s, job y), thread = (claim, 4-channel chunk), strided.  k_rows_commit then
 // advances the row counter (a claim past the capacity is undone: map -1; the counter
 // keeps the overshoot, which the caller checks).
 // ---------------------------------------------------------------------------
@@ -63,13 +63,15 @@ __global__ void __launch_bounds__(256) k_rows_compact(const MlpCtx m) {
   if (!G.grad_rows) return;
   const int32_t* cnt = m.claim_cnt + y * CLAIM_SHARDS;
   const int64_t n = min((int64_t)cnt[s], m.claim_cap);
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (claim, 4-channel chunk)
-  if (e >= n * 8) return;
-  int64_t prefix = 0;
-  for (int t = 0; t < s; ++t) prefix += min((int64_t)cnt[t], m.claim_cap);
-  const int64_t base = (int64_t)*G.row_count + prefix;
+  if ((int64_t)blockIdx.x * blockDim.x >= n * 8) return;  // block past this shard's claims
+  // rows before this shard: a wave sum over the shard counters (lane t < s holds shard t)
+  const int lane = threadIdx.x & 63;
+  int part = lane < s ? (int)min((int64_t)cnt[lane], m.claim_cap) : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+  const int64_t base = (int64_t)*G.row_count + part;
   const int64_t* tmp = m.claim_tmp + ((int64_t)y * CLAIM_SHARDS + s) * m.claim_cap;
-  {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * 8; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t l = e >> 3;
     const int c = (int)(e & 7);
     const int64_t v = tmp[l], r = base + l;
@@ -96,8 +98,8 @@ __global__ void k_rows_commit(const MlpCtx m) {
 }
 
 int launch_rows_compact(const MlpCtx& m, hipStream_t s) {
-  // one thread per (claim, chunk) of a full shard; blocks past a shard's count exit at once
-  const int64_t bx = (m.claim_cap * 8 + 255) / 256;
+  // (claim, chunk) items of a shard strided over bx blocks (a full shard: 8 claim_cap items)
+  const int64_t bx = std::min<int64_t>((m.claim_cap * 8 + 255) / 256, 16);
   hipLaunchKernelGGL(k_rows_compact, dim3((unsigned)bx, CLAIM_SHARDS, m.n_jobs), dim3(256), 0, s, m);
   if (hipError_t e = hipGetLastError()) return (int)e;
   hipLaunchKernelGGL(k_rows_commit, dim3(1), dim3(64), 0, s, m);
