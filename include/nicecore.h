@@ -20,6 +20,8 @@
  *                       pose gradient (Tracker.py:95-111, Mapper.py:543-591).
  *   nc_frustum_mask     src/Mapper.py:100-187 get_mask_from_c2w (frustum feature
  *                       selection of one grid).
+ *   nc_sample_pdf       src/common.py:19-63 sample_pdf (importance sampling,
+ *                       Renderer.py:244-250 when N_importance > 0).
  *   nc_sparse_rows_*    the touched-voxel gradient of a feature grid too large for a
  *                       dense gradient: the reference's dense
  *                       grid.grad / val[mask] gradient (Mapper.py:392-404, :620-627)
@@ -268,6 +270,31 @@ typedef struct nc_frustum_args {
 
 int nc_frustum_mask(const nc_frustum_args* args, void* stream);
 
+/* Hierarchical (importance) sampling, sample_pdf (src/common.py:19-63), as
+ * render_batch_ray applies it when N_importance > 0 (src/utils/Renderer.py:244-250):
+ * per ray, N inverse-CDF samples of the piecewise-constant pdf weights + 1e-5 over
+ * bins (float64 [n_rays][n_bins], the mid-points of the sorted sample depths;
+ * weights float32 [n_rays][n_bins - 1]).  u = linspace(0, 1, N) when det, else the
+ * caller's uniform draw (float32 [n_rays][N]).  n_bins, N <= NC_MAX_SAMPLES.
+ * (ABI v5) */
+typedef struct nc_pdf_args {
+  int32_t abi_version;
+  int32_t det;             /* 1: u = torch.linspace(0, 1, n_samples) */
+  int64_t n_rays;
+  int64_t n_bins;          /* >= 2 */
+  int64_t n_samples;       /* N_importance */
+  const double* bins;      /* [n_rays][n_bins], row stride bins_stride */
+  int64_t bins_stride;
+  const float* weights;    /* [n_rays][n_bins - 1], row stride weights_stride */
+  int64_t weights_stride;
+  const float* u;          /* [n_rays][n_samples] or NULL (det) */
+  int64_t u_stride;
+  double* samples;         /* [n_rays][n_samples] output */
+  int64_t samples_stride;
+} nc_pdf_args;
+
+int nc_sample_pdf(const nc_pdf_args* args, void* stream);
+
 /* Sparse gradient rows of one grid (ABI v5; see nc_grid). */
 typedef struct nc_sparse_rows {
   int32_t* grad_rows;   /* [n_voxels] voxel -> row map */
@@ -303,7 +330,7 @@ int64_t nc_param_count(int decoder);
 
 /* sizeof() of the ABI structs, for binding-layout checks:
  * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params, 4 nc_sample_args, 5 nc_frustum_args,
- * 6 nc_sparse_rows. */
+ * 6 nc_sparse_rows, 7 nc_pdf_args. */
 size_t nc_struct_size(int which);
 
 size_t nc_render_workspace_bytes(const nc_render_args* args);

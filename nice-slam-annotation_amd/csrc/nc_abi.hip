@@ -37,13 +37,13 @@ enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
   KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
-  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_COUNT
+  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
-                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce"};
+                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce", "k_sample_pdf"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -565,6 +565,7 @@ size_t nc_struct_size(int which) {
     case 4: return sizeof(nc_sample_args);
     case 5: return sizeof(nc_frustum_args);
     case 6: return sizeof(nc_sparse_rows);
+    case 7: return sizeof(nc_pdf_args);
   }
   return 0;
 }
@@ -746,6 +747,19 @@ int nc_frustum_mask(const nc_frustum_args* a, void* stream) {
   if (a->H > 32767 || a->W > 32767) return fail(-1, "nicecore: cv2.remap semantics need H, W < 32768");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return check_hip(timed(KID_FRUSTUM, s, [&] { return launch_frustum_mask(*a, s); }), "k_frustum_mask");
+}
+
+int nc_sample_pdf(const nc_pdf_args* a, void* stream) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (a->n_rays < 0) return fail(-1, "nicecore: n_rays < 0");
+  if (a->n_bins < 2 || a->n_bins > NC_MAX_SAMPLES || a->n_samples < 1 || a->n_samples > NC_MAX_SAMPLES)
+    return fail(-1, "nicecore: sample_pdf needs 2 <= n_bins <= 64 and 1 <= n_samples <= 64");
+  if (a->n_rays == 0) return 0;
+  if (!a->bins || !a->weights || !a->samples || (!a->det && !a->u))
+    return fail(-1, "nicecore: NULL bins, weights, samples or (det = 0) u");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_SAMPLE_PDF, s, [&] { return launch_sample_pdf(*a, s); }), "k_sample_pdf");
 }
 
 static int rows_check(const nc_sparse_rows* r, const char* what) {

@@ -95,6 +95,13 @@ class NcSparseRows(ctypes.Structure):
                 ("row_count", c_void_p), ("capacity", c_int64), ("values", c_void_p)]
 
 
+class NcPdfArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("det", c_int32), ("n_rays", c_int64), ("n_bins", c_int64),
+                ("n_samples", c_int64), ("bins", c_void_p), ("bins_stride", c_int64),
+                ("weights", c_void_p), ("weights_stride", c_int64), ("u", c_void_p), ("u_stride", c_int64),
+                ("samples", c_void_p), ("samples_stride", c_int64)]
+
+
 EXPORTS = {
     "nc_abi_version": (c_int, []),
     "nc_last_error": (ctypes.c_char_p, []),
@@ -112,6 +119,7 @@ EXPORTS = {
     "nc_sample_rays_forward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
     "nc_sample_rays_backward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
     "nc_frustum_mask": (c_int, [POINTER(NcFrustumArgs), c_void_p]),
+    "nc_sample_pdf": (c_int, [POINTER(NcPdfArgs), c_void_p]),
     "nc_sparse_rows_clear": (c_int, [POINTER(NcSparseRows), c_void_p]),
     "nc_sparse_merge_temp_bytes": (c_size_t, [c_int64, c_int64]),
     "nc_sparse_rows_merge": (c_int, [POINTER(NcSparseRows), POINTER(NcSparseRows), c_void_p, c_void_p,
@@ -158,7 +166,7 @@ KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_f
               "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15,
               "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18,
               "k_rows_clear": 19, "k_rows_merge": 20, "k_rows_compact": 21,
-              "k_param_ray_reduce": 22}
+              "k_param_ray_reduce": 22, "k_sample_pdf": 23}
 
 
 class KernelTimer:

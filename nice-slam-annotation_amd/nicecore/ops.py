@@ -88,3 +88,36 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
             "deterministic": deterministic, "sparse": sparse_grads,
             "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth, target_color if color_term else None)}
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
+
+
+def sample_pdf(bins, weights, N_samples, det=False, device=None, u=None):
+    """Hierarchical sampling (src/common.py:19-63) on the HIP core (``nc_sample_pdf``):
+    ``N_samples`` inverse-CDF samples per row of the piecewise-constant pdf
+    ``weights + 1e-5`` over ``bins``.  ``bins`` [..., nb] float64 (the reference passes
+    the mid-points of its float64 sample depths), ``weights`` [..., nb - 1] float32.
+    ``det=False`` draws ``u`` uniformly on the device unless it is given (the reference
+    draws it with ``torch.rand`` on the CPU).  Returns float64 [..., N_samples]; no
+    gradient (the reference detaches the samples, Renderer.py:247)."""
+    import ctypes
+    lib = L.load()
+    dev = bins.device
+    if dev.type != "cuda":
+        raise L.NiceCoreError("sample_pdf runs on a HIP device; bins are on " + str(dev))
+    lead = bins.shape[:-1]
+    nb = bins.shape[-1]
+    b = bins.detach().reshape(-1, nb).to(torch.float64).contiguous()
+    w = weights.detach().reshape(-1, weights.shape[-1]).to(torch.float32).contiguous()
+    if w.shape != (b.shape[0], nb - 1):
+        raise L.NiceCoreError(f"weights must be [..., {nb - 1}] for {nb} bins, got {tuple(weights.shape)}")
+    n = b.shape[0]
+    uu = None
+    if not det:
+        uu = (torch.rand(n, N_samples, device=dev) if u is None
+              else u.detach().reshape(n, N_samples).to(device=dev, dtype=torch.float32).contiguous())
+    out = torch.empty(n, N_samples, device=dev, dtype=torch.float64)
+    a = L.NcPdfArgs(abi_version=L.NC_ABI_VERSION, det=1 if det else 0, n_rays=n, n_bins=nb,
+                    n_samples=N_samples, bins=b.data_ptr(), bins_stride=nb, weights=w.data_ptr(),
+                    weights_stride=nb - 1, u=uu.data_ptr() if uu is not None else None,
+                    u_stride=N_samples, samples=out.data_ptr(), samples_stride=N_samples)
+    L.check(lib.nc_sample_pdf(ctypes.byref(a), torch.cuda.current_stream(dev).cuda_stream), "nc_sample_pdf")
+    return out.reshape(*lead, N_samples)

@@ -42,6 +42,7 @@ def test_struct_layouts_match(lib):
     assert lib.nc_struct_size(4) == ctypes.sizeof(L.NcSampleArgs)
     assert lib.nc_struct_size(5) == ctypes.sizeof(L.NcFrustumArgs)
     assert lib.nc_struct_size(6) == ctypes.sizeof(L.NcSparseRows)
+    assert lib.nc_struct_size(7) == ctypes.sizeof(L.NcPdfArgs)
     assert lib.nc_abi_version() == L.NC_ABI_VERSION
 
 
