@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 5
+#define NC_ABI_VERSION 6
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -175,6 +175,17 @@ typedef struct nc_render_args {
    * of 4 floats). */
   float* grad_zero;
   int64_t grad_zero_floats;
+  /* hierarchical sampling, N_importance > 0 (ABI v6; src/utils/Renderer.py:239-259):
+   * the first pass writes its sorted sample depths and compositing weights (z_out,
+   * weights_out: [N][S]); sample_pdf (nc_sample_pdf) draws N_importance depths from
+   * them; the second pass takes those as z_extra ([N][n_extra], no gradient) and
+   * renders the sorted union of its own samples and them (S = n_strat + n_surf +
+   * n_extra <= NC_MAX_SAMPLES). */
+  const double* z_extra;
+  int32_t n_extra;
+  int32_t reserved3;
+  double* z_out;
+  float* weights_out;
 } nc_render_args;
 
 typedef struct nc_points_args {

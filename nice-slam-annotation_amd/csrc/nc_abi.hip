@@ -373,11 +373,14 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
   if (int e = plan_stage(a->stage, pl)) return e;
   if (a->n_rays < 0) return fail(-1, "nicecore: n_rays < 0");
-  if (a->n_strat < 1 || a->n_surf < 0 || a->n_surf > NC_MAX_SURF || a->n_strat + a->n_surf > NC_MAX_SAMPLES)
-    return fail(-1, "nicecore: need 1 <= N_samples, 0 <= N_surface <= 32, N_samples + N_surface <= 64");
+  if (a->n_extra < 0 || (a->n_extra > 0 && !a->z_extra && a->n_rays > 0))
+    return fail(-1, "nicecore: n_extra > 0 needs z_extra");
+  if (a->n_strat < 1 || a->n_surf < 0 || a->n_surf > NC_MAX_SURF ||
+      a->n_strat + a->n_surf + a->n_extra > NC_MAX_SAMPLES)
+    return fail(-1, "nicecore: need 1 <= N_samples, 0 <= N_surface <= 32, N_samples + N_surface + n_extra <= 64");
   if (a->n_surf > 0 && !a->gt_depth && a->n_rays > 0) return fail(-1, "nicecore: N_surface > 0 requires gt_depth");
   if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
-  S = a->n_strat + a->n_surf;
+  S = a->n_strat + a->n_surf + a->n_extra;
   P = a->n_rays * S;
   if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC | NC_SAVE_POINT_JACOBIAN)) return fail(-1, "nicecore: unknown flags");
   if (a->loss < NC_LOSS_NONE || a->loss > NC_LOSS_TRACKER) return fail(-1, "nicecore: unknown loss " + std::to_string(a->loss));
@@ -410,6 +413,10 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
   c.S = S;
   c.n_strat = a->n_strat;
   c.n_surf = a->n_surf;
+  c.n_extra = a->n_extra;
+  c.z_extra = a->z_extra;
+  c.z_out = a->z_out;
+  c.weights_out = a->weights_out;
   c.stage = a->stage;
   c.occ_a = pl.occ_a;
   c.occ_b = pl.occ_b;

@@ -105,6 +105,10 @@ struct RayCtx {
   int64_t P;
   int32_t S;             // samples per ray
   int32_t n_strat, n_surf;
+  int32_t n_extra;       // caller depths merged into the samples (importance pass)
+  const double* z_extra; // [N][n_extra]
+  double* z_out;         // optional [N][S] sorted sample depths
+  float* weights_out;    // optional [N][S] compositing weights
   int32_t stage;
   int32_t occ_a, occ_b;  // occupancy slots summed into raw[...,3] (-1: none)
   int32_t has_rgb;

@@ -111,10 +111,12 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
     } else {         // Renderer.py:193-196
       z = 0.001 * (1.0 - ts) + (double)dmax * ts;
     }
+  } else if (lane < c.S) {  // importance samples (Renderer.py:248: sorted with the rest)
+    z = c.z_extra[r * c.n_extra + (lane - c.n_strat - c.n_surf)];
   } else {
     z = INFINITY;
   }
-  if (c.n_surf > 0) {  // Renderer.py:222-224 torch.sort of the 48 depths (bitonic, 64 lanes)
+  if (c.n_surf > 0 || c.n_extra > 0) {  // Renderer.py:222-224 / :248 torch.sort (bitonic, 64 lanes)
 #pragma unroll
     for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
@@ -131,6 +133,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   if (lane < c.S) {
     const int64_t p = r * c.S + lane;
     c.z[p] = z;
+    if (c.z_out) c.z_out[p] = z;
     double pt[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -230,6 +233,7 @@ __global__ void __launch_bounds__(256) k_composite_fwd(const RayCtx c) {
   const double depth = wsum_d((double)s.w * s.z);
   const double tmp = s.z - depth;
   const double var = wsum_d(lane < c.S ? ((double)s.w * tmp) * tmp : 0.0);
+  if (c.weights_out && lane < c.S) c.weights_out[r * c.S + lane] = s.w;
   if (lane == 0) {
     c.depth[r] = depth;
     c.var[r] = var;

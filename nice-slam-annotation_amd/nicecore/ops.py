@@ -21,8 +21,31 @@ def eval_points(decoders, p, c_grid, stage='middle', deterministic=None, sparse_
     return NiceEvalFn.apply(spec, p, *_grid_args(c_grid), *plan.flat_params())
 
 
+def _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, n_surf,
+                       depth_max, n_importance, det):
+    """Renderer.py:239-250: a forward-only first pass over the stratified (+ surface)
+    samples, then sample_pdf over its weights without the first and last sample at the
+    mid-points of its depths.  Returns the N_importance depths [N, n_importance]."""
+    N = rays_o.shape[0]
+    S = n_strat + n_surf
+    dev = rays_o.device
+    z = torch.empty(N, S, device=dev, dtype=torch.float64)
+    w = torch.empty(N, S, device=dev, dtype=torch.float32)
+    plan = make_plan(stage, decoders)
+    spec = {"plan": plan, "n_strat": n_strat, "n_surf": n_surf, "bound": bound, "depth_max": depth_max,
+            "z_out": z, "weights_out": w}
+    with torch.no_grad():
+        grids = [g.detach() if g is not None else None for g in _grid_args(c)]
+        NiceRenderFn.apply(spec, rays_o.detach(), rays_d.detach(),
+                           gt_depth.detach() if gt_depth is not None else None, *grids,
+                           *[p.detach() for p in plan.flat_params()])
+        z_mid = .5 * (z[..., 1:] + z[..., :-1])
+        return sample_pdf(z_mid, w[..., 1:-1], n_importance, det=det)
+
+
 def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_strat=32,
-                n_surf=16, depth_max=None, deterministic=None, sparse_grads=None):
+                n_surf=16, depth_max=None, deterministic=None, sparse_grads=None, n_importance=0,
+                perturb=0.):
     """Renderer.render_batch_ray core (src/utils/Renderer.py:95-262) with
     N_importance = 0, lindisp = False, perturb = 0, occupancy = True.
     Returns (depth float64 [N], uncertainty float64 [N], color float32 [N,3]).
@@ -35,15 +58,22 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     ``NC_DETERMINISTIC=1`` or ``torch.use_deterministic_algorithms(True)``.
 
     ``sparse_grads``: a ``nicecore.sparse.SparseGridGrads``; the grids it covers get
-    their gradient as touched-voxel rows there instead of a dense ``.grad``."""
+    their gradient as touched-voxel rows there instead of a dense ``.grad``.
+
+    ``n_importance`` > 0: hierarchical sampling (Renderer.py:239-259) -- a forward-only
+    pass, ``sample_pdf`` (deterministic u when ``perturb`` == 0, as the reference), and
+    the differentiable render over the sorted union of both sample sets."""
     if stage == 'coarse':
         gt_depth = None
     ns = n_surf if gt_depth is not None else 0
-    if n_strat + ns > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
-        raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
+    if n_strat + ns + n_importance > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
+        raise L.NiceCoreError("nicecore supports N_samples + N_surface + N_importance <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
             "deterministic": deterministic, "sparse": sparse_grads}
+    if n_importance > 0:
+        spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
+                                             depth_max, n_importance, det=(perturb == 0.))
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
 
 
@@ -53,7 +83,7 @@ _LOSS_KINDS = {"mapper": L.NC_LOSS_MAPPER, "tracker": L.NC_LOSS_TRACKER}
 def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, loss="mapper",
                      target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
                      gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None,
-                     sparse_grads=None):
+                     sparse_grads=None, n_importance=0, perturb=0.):
     """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
     color, loss) with ``loss`` a float64 device scalar that backpropagates into the
     grids / decoders / rays like the reference's loss expression:
@@ -81,12 +111,15 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
     if stage == 'coarse':
         gt_depth = None
     ns = n_surf if gt_depth is not None else 0
-    if n_strat + ns > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
-        raise L.NiceCoreError("nicecore supports N_samples + N_surface <= 64 (N_surface <= 32)")
+    if n_strat + ns + n_importance > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
+        raise L.NiceCoreError("nicecore supports N_samples + N_surface + N_importance <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
             "deterministic": deterministic, "sparse": sparse_grads,
             "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth, target_color if color_term else None)}
+    if n_importance > 0:
+        spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
+                                             depth_max, n_importance, det=(perturb == 0.))
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
 
 

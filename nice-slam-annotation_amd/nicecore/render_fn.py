@@ -404,6 +404,16 @@ class NiceRenderFn(torch.autograd.Function):
         if dmax is not None:
             dmax = dmax.detach().reshape(1).float().contiguous()
             a.depth_max = dmax.data_ptr()
+        # hierarchical sampling (Renderer.py:239-259): pass 1 reports its depths and
+        # weights, pass 2 merges the sample_pdf depths (no gradient) into its samples
+        zx = spec.get("z_extra")
+        if zx is not None:
+            zx = zx.detach().double().contiguous()
+            a.z_extra, a.n_extra = zx.data_ptr(), zx.shape[-1]
+        for name in ("z_out", "weights_out"):
+            t = spec.get(name)
+            if t is not None:
+                setattr(a, name, t.data_ptr())
         grids = (g0, g1, g2, g3)
         gkeep = []
         for k in plan.grids:
@@ -413,7 +423,7 @@ class NiceRenderFn(torch.autograd.Function):
             _fill_grid(a.grids[k], g, device)
             gkeep.append(g)
         if a.flags & L.NC_SAVE_FOR_BACKWARD:
-            _bind_sparse(sparse, a, plan, N * (spec["n_strat"] + spec["n_surf"]))
+            _bind_sparse(sparse, a, plan, N * (spec["n_strat"] + spec["n_surf"] + a.n_extra))
         depth = torch.empty(N, device=device, dtype=torch.float64)
         var = torch.empty(N, device=device, dtype=torch.float64)
         color = torch.empty(N, 3, device=device, dtype=torch.float32)
@@ -447,7 +457,8 @@ class NiceRenderFn(torch.autograd.Function):
         a.grad_zero, a.grad_zero_floats = None, 0
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
         ctx.sparse = sparse
-        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt)
+        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt, zx)
+        a.z_out, a.weights_out = None, None  # pass-1 outputs: not rewritten by the backward
         ctx.grids = grids
         if loss is None:
             return depth, var, color

@@ -13,9 +13,9 @@ src/Tracker.py / src/Mapper.py / src/utils/Visualizer.py call it unchanged:
 plus ``render_batch_loss`` (extension): render_batch_ray with the Mapper's / Tracker's
 loss expression (Mapper.py:603-612, Tracker.py:117-131) computed in the same launches.
 
-Only the configuration the NICE configs use is implemented (N_importance = 0,
-lindisp = False, perturb = 0, occupancy = True; configs/nice_slam.yaml:5,121-126);
-anything else raises instead of silently falling back.
+Implemented: the NICE decoders with lindisp = False, perturb = 0, occupancy = True
+(configs/nice_slam.yaml:5,121-126) and any N_importance (hierarchical sampling,
+Renderer.py:239-259); anything else raises instead of silently falling back.
 """
 from __future__ import annotations
 
@@ -46,9 +46,9 @@ class Renderer(object):
     def _check_supported(self):
         if not self.nice:
             raise NotImplementedError("nicecore renders NICE decoders only (iMAP* is out of scope)")
-        if self.N_importance > 0 or self.lindisp or self.perturb > 0. or not self.occupancy:
+        if self.lindisp or self.perturb > 0. or not self.occupancy:
             raise NotImplementedError(
-                "nicecore implements N_importance=0, lindisp=False, perturb=0, occupancy=True")
+                "nicecore implements lindisp=False, perturb=0, occupancy=True (N_importance >= 0)")
 
     def eval_points(self, p, decoders, c=None, stage='color', device='cuda:0'):
         """Renderer.py:36-93: NICE.forward plus the strict in-bound mask; points outside
@@ -74,7 +74,8 @@ class Renderer(object):
         if gt_depth is not None:
             gt_depth = gt_depth.reshape(-1)
         return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
-                           self.N_samples, self.N_surface, depth_max, sparse_grads=sparse_grads)
+                           self.N_samples, self.N_surface, depth_max, sparse_grads=sparse_grads,
+                           n_importance=self.N_importance, perturb=self.perturb)
 
     def render_batch_loss(self, c, decoders, rays_d, rays_o, device, stage, gt_depth, gt_color=None,
                           loss='mapper', w_color_loss=0.2, color_term=False, handle_dynamic=False,
@@ -88,7 +89,8 @@ class Renderer(object):
         return render_rays_loss(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth.reshape(-1),
                                 loss, gt_color, w_color_loss, color_term, handle_dynamic,
                                 render_gt_depth, self.N_samples, self.N_surface, depth_max,
-                                sparse_grads=sparse_grads)
+                                sparse_grads=sparse_grads, n_importance=self.N_importance,
+                                perturb=self.perturb)
 
     def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
         """Renderer.py:264-340: chunked full-image render, no grad."""

@@ -175,8 +175,9 @@ def composite(raw, z_vals):
 
 
 def render_batch_ray(grids, prm, dec_bounds, bound, rays_d, rays_o, stage, gt_depth=None,
-                     n_strat=32, n_surf=16, depth_max=None):
-    """Renderer.py:95-262 (N_importance = 0, lindisp/perturb off, occupancy on).
+                     n_strat=32, n_surf=16, depth_max=None, n_importance=0):
+    """Renderer.py:95-262 (lindisp/perturb off, occupancy on; hierarchical sampling with
+    sample_pdf, :239-259, when n_importance > 0).
     Returns (depth f64 [N], uncertainty f64 [N], color f32 [N,3])."""
     if stage == 'coarse':
         gt_depth = None
@@ -185,7 +186,16 @@ def render_batch_ray(grids, prm, dec_bounds, bound, rays_d, rays_o, stage, gt_de
     pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
     raw = eval_points(pts.reshape(-1, 3), grids, prm, bound, dec_bounds, stage)
     raw = raw.reshape(rays_o.shape[0], S, -1)
-    depth, var, color, _ = composite(raw, z)
+    depth, var, color, weights = composite(raw, z)
+    if n_importance > 0:
+        from oracle.pdf_oracle import sample_pdf
+        z_mid = .5 * (z[..., 1:] + z[..., :-1])
+        z_samples = sample_pdf(z_mid, weights[..., 1:-1], n_importance, det=True).detach()
+        z, _ = torch.sort(torch.cat([z, z_samples], -1), -1)
+        pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
+        raw = eval_points(pts.reshape(-1, 3), grids, prm, bound, dec_bounds, stage)
+        raw = raw.reshape(rays_o.shape[0], S + n_importance, -1)
+        depth, var, color, _ = composite(raw, z)
     return depth, var, color
 
 

@@ -81,7 +81,8 @@ CASES = [
 ]
 
 
-def main():
+def setup():
+    """The tiny scene, the reference's model and grids as main() builds them."""
     ref_config, RefRenderer, cfg = _import_reference()
     scene = S.make_scene("tiny")
     cfg['mapping']['bound'] = S.PRESETS["tiny"]["bound"]
@@ -112,6 +113,11 @@ def main():
 
     slam = types.SimpleNamespace(nice=True, bound=bound, H=scene.H, W=scene.W, fx=scene.fx,
                                  fy=scene.fy, cx=scene.cx, cy=scene.cy)
+    return ref_config, RefRenderer, cfg, scene, model, grids_big, bound, slam
+
+
+def main():
+    ref_config, RefRenderer, cfg, scene, model, grids_big, bound, slam = setup()
     renderer = RefRenderer(cfg, None, slam)
 
     sc = {
