@@ -24,6 +24,7 @@ VARIANTS = {
     "dx_no_coord": ["-DNC_ABL_DX_NO_COORD"],
     "dx_no_trilinear": ["-DNC_ABL_DX_NO_SCATTER", "-DNC_ABL_DX_NO_COORD"],
     "dx512": ["-DNC_DX_THREADS=512"],
+    "no_sort": ["-DNC_ABL_NO_SORT"],
     "dw512_16": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=16"],
     "dw256_16": ["-DNC_DW_THREADS=256", "-DNC_DW_NPTS=16"],
     "dw1024_16": ["-DNC_DW_THREADS=1024", "-DNC_DW_NPTS=16"],
