@@ -20,6 +20,7 @@
  *                       pose gradient (Tracker.py:95-111, Mapper.py:543-591).
  *   nc_frustum_mask     src/Mapper.py:100-187 get_mask_from_c2w (frustum feature
  *                       selection of one grid).
+ *   nc_adam_step        torch.optim.Adam / SparseAdam step (src/Mapper.py:462-485, :625)
  *   nc_sample_pdf       src/common.py:19-63 sample_pdf (importance sampling,
  *                       Renderer.py:244-250 when N_importance > 0).
  *   nc_sparse_rows_*    the touched-voxel gradient of a feature grid too large for a
@@ -54,7 +55,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 6
+#define NC_ABI_VERSION 7
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -333,6 +334,38 @@ int nc_sparse_rows_merge(const nc_sparse_rows* in, const nc_sparse_rows* out, co
                          const int32_t* all_count, int32_t world, int64_t rank_capacity, void* temp,
                          size_t temp_bytes, void* stream);
 
+/* Optimiser step of the Mapper (torch.optim.Adam over the grids and the colour decoder,
+ * src/Mapper.py:462-485 param groups, :625 optimizer.step()).  (ABI v7)
+ *   NC_ADAM_DENSE: param/grad/exp_avg/exp_avg_sq are n contiguous floats; the arithmetic of
+ *     torch.optim.Adam(fused=True) (ATen fused_adam_utils.cuh adam_math: ORIGINAL mode,
+ *     weight_decay added to the gradient, no amsgrad / maximize).  step = the step count
+ *     after its increment (1 at the first step).
+ *   NC_ADAM_SPARSE_ROWS: torch.optim.SparseAdam's rule (torch/optim/_functional.py
+ *     sparse_adam) on the rows of a sparse grid gradient (nc_sparse_rows): grad = the
+ *     [row_capacity][32] values, row_voxel / *row_count the touched voxels; param and
+ *     moments addressed as voxel * voxel_stride + channel * channel_stride.  Untouched
+ *     voxels are left as they are (lazy).  weight_decay must be 0, as SparseAdam has none. */
+#define NC_ADAM_DENSE 0
+#define NC_ADAM_SPARSE_ROWS 1
+typedef struct nc_adam_args {
+  int32_t abi_version;
+  int32_t mode;               /* NC_ADAM_* */
+  int64_t n;                  /* dense: number of elements */
+  float* param;
+  const float* grad;          /* dense: [n]; rows: [row_capacity][32] */
+  float* exp_avg;
+  float* exp_avg_sq;
+  const int64_t* row_voxel;   /* rows: [row_capacity] */
+  const int32_t* row_count;   /* rows: device scalar */
+  int64_t row_capacity;
+  int64_t voxel_stride;       /* rows: channels-last 32, NCDHW 1 */
+  int64_t channel_stride;     /* rows: channels-last 1, NCDHW D*H*W */
+  double lr, beta1, beta2, eps, weight_decay;
+  double step;
+} nc_adam_args;
+
+int nc_adam_step(const nc_adam_args* args, void* stream);
+
 int nc_abi_version(void);
 const char* nc_last_error(void);
 
@@ -341,7 +374,7 @@ int64_t nc_param_count(int decoder);
 
 /* sizeof() of the ABI structs, for binding-layout checks:
  * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params, 4 nc_sample_args, 5 nc_frustum_args,
- * 6 nc_sparse_rows, 7 nc_pdf_args. */
+ * 6 nc_sparse_rows, 7 nc_pdf_args, 8 nc_adam_args. */
 size_t nc_struct_size(int which);
 
 size_t nc_render_workspace_bytes(const nc_render_args* args);

@@ -37,13 +37,13 @@ enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
   KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
-  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_COUNT
+  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_ADAM, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
-                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce", "k_sample_pdf"};
+                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce", "k_sample_pdf", "k_adam"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -573,6 +573,7 @@ size_t nc_struct_size(int which) {
     case 5: return sizeof(nc_frustum_args);
     case 6: return sizeof(nc_sparse_rows);
     case 7: return sizeof(nc_pdf_args);
+    case 8: return sizeof(nc_adam_args);
   }
   return 0;
 }
@@ -767,6 +768,30 @@ int nc_sample_pdf(const nc_pdf_args* a, void* stream) {
     return fail(-1, "nicecore: NULL bins, weights, samples or (det = 0) u");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return check_hip(timed(KID_SAMPLE_PDF, s, [&] { return launch_sample_pdf(*a, s); }), "k_sample_pdf");
+}
+
+int nc_adam_step(const nc_adam_args* a, void* stream) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (!(a->step >= 1.0)) return fail(-1, "nicecore: adam step count must be >= 1");
+  if (!(a->beta1 >= 0.0 && a->beta1 < 1.0 && a->beta2 >= 0.0 && a->beta2 < 1.0 && a->eps >= 0.0 && a->lr >= 0.0))
+    return fail(-1, "nicecore: adam needs 0 <= beta < 1, eps >= 0, lr >= 0");
+  if (a->mode == NC_ADAM_DENSE) {
+    if (a->n < 0) return fail(-1, "nicecore: adam n < 0");
+    if (a->n > 0 && (!a->param || !a->grad || !a->exp_avg || !a->exp_avg_sq))
+      return fail(-1, "nicecore: adam: NULL param, grad or moment");
+  } else if (a->mode == NC_ADAM_SPARSE_ROWS) {
+    if (a->row_capacity < 0) return fail(-1, "nicecore: adam row_capacity < 0");
+    if (a->weight_decay != 0.0) return fail(-1, "nicecore: the sparse-rows rule (SparseAdam) has no weight_decay");
+    if (!a->row_count || (a->row_capacity > 0 && (!a->param || !a->grad || !a->exp_avg || !a->exp_avg_sq ||
+                                                    !a->row_voxel)))
+      return fail(-1, "nicecore: adam: NULL param, rows, moment or row count");
+    if (a->voxel_stride < 1 || a->channel_stride < 1) return fail(-1, "nicecore: adam: bad voxel/channel stride");
+  } else {
+    return fail(-1, "nicecore: unknown adam mode");
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_ADAM, s, [&] { return launch_adam(*a, s); }), "k_adam");
 }
 
 static int rows_check(const nc_sparse_rows* r, const char* what) {

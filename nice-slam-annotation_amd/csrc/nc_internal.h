@@ -91,6 +91,8 @@ int launch_sample_pose_grad(const nc_sample_args& a, hipStream_t s);
 int launch_frustum_mask(const nc_frustum_args& a, hipStream_t s);
 // importance sampling (nc_pdf.hip)
 int launch_sample_pdf(const nc_pdf_args& a, hipStream_t s);
+// optimiser step (nc_adam.hip)
+int launch_adam(const nc_adam_args& a, hipStream_t s);
 // sparse gradient rows (nc_sparse.hip)
 int launch_rows_clear(const nc_sparse_rows& r, hipStream_t s);
 int launch_rows_compact(const MlpCtx& m, hipStream_t s);  // after k_grid_gather's claims

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 6
+NC_ABI_VERSION = 7
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
 NC_SAVE_POINT_JACOBIAN = 4
@@ -104,6 +104,17 @@ class NcPdfArgs(ctypes.Structure):
                 ("samples", c_void_p), ("samples_stride", c_int64)]
 
 
+class NcAdamArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("mode", c_int32), ("n", c_int64), ("param", c_void_p),
+                ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p), ("row_voxel", c_void_p),
+                ("row_count", c_void_p), ("row_capacity", c_int64), ("voxel_stride", c_int64),
+                ("channel_stride", c_int64), ("lr", c_double), ("beta1", c_double), ("beta2", c_double),
+                ("eps", c_double), ("weight_decay", c_double), ("step", c_double)]
+
+
+NC_ADAM_DENSE = 0
+NC_ADAM_SPARSE_ROWS = 1
+
 EXPORTS = {
     "nc_abi_version": (c_int, []),
     "nc_last_error": (ctypes.c_char_p, []),
@@ -122,6 +133,7 @@ EXPORTS = {
     "nc_sample_rays_backward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
     "nc_frustum_mask": (c_int, [POINTER(NcFrustumArgs), c_void_p]),
     "nc_sample_pdf": (c_int, [POINTER(NcPdfArgs), c_void_p]),
+    "nc_adam_step": (c_int, [POINTER(NcAdamArgs), c_void_p]),
     "nc_sparse_rows_clear": (c_int, [POINTER(NcSparseRows), c_void_p]),
     "nc_sparse_merge_temp_bytes": (c_size_t, [c_int64, c_int64]),
     "nc_sparse_rows_merge": (c_int, [POINTER(NcSparseRows), POINTER(NcSparseRows), c_void_p, c_void_p,
@@ -168,7 +180,7 @@ KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_f
               "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15,
               "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18,
               "k_rows_clear": 19, "k_rows_merge": 20, "k_rows_compact": 21,
-              "k_param_ray_reduce": 22, "k_sample_pdf": 23}
+              "k_param_ray_reduce": 22, "k_sample_pdf": 23, "k_adam": 24}
 
 
 class KernelTimer:

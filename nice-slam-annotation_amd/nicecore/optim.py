@@ -1,0 +1,148 @@
+"""The Mapper's optimiser step on the device (nc_adam_step, include/nicecore.h ABI v7).
+
+``Adam`` is a drop-in for the ``torch.optim.Adam`` the Mapper builds over its decoder
+parameters and feature grids (src/Mapper.py:462-485: one param group per decoder set /
+grid with its own lr, StepLR on top; :625 ``optimizer.step()``).  Its update is the
+arithmetic of ``torch.optim.Adam(fused=True)`` (ATen fused_adam_utils.cuh): one
+``k_adam_dense`` launch per parameter reads param/grad/moments once and writes
+param/moments once (28 B per element, HBM-bound), for grids in either memory format.
+State (``step``, ``exp_avg``, ``exp_avg_sq``) and ``state_dict`` follow torch.optim.Adam,
+so schedulers and checkpoints keep working.
+
+``SparseGridAdam`` steps the grids whose gradient lives in ``SparseGridGrads`` rows
+(C5): ``torch.optim.SparseAdam``'s rule (torch/optim/_functional.py
+sparse_adam) on the touched voxels only, with the moments kept in the grid's own
+layout.  After ``SparseGridGrads.allreduce`` every rank holds the same union and the
+same summed rows, so replicated grids stay identical.
+
+There is no CPU path: the step needs libnicecore.so and a HIP device.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+
+def _dense_layout(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense (any dimension order): a flat [numel] view of its storage."""
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
+def _adam_args(mode, lr, beta1, beta2, eps, weight_decay, step) -> L.NcAdamArgs:
+    a = L.NcAdamArgs()
+    a.abi_version = L.NC_ABI_VERSION
+    a.mode = mode
+    a.lr, a.beta1, a.beta2 = float(lr), float(beta1), float(beta2)
+    a.eps, a.weight_decay, a.step = float(eps), float(weight_decay), float(step)
+    return a
+
+
+def adam_step_(param, grad, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weight_decay, step):
+    """One fused Adam update of ``param`` / ``exp_avg`` / ``exp_avg_sq`` in place
+    (torch.optim.Adam(fused=True) arithmetic; ``step`` counted from 1).  All four
+    tensors: float32 on one HIP device, same shape and strides, non-overlapping and dense."""
+    ts = (param, grad, exp_avg, exp_avg_sq)
+    for t in ts:
+        if t.dtype != torch.float32 or t.device.type != "cuda":
+            raise L.NiceCoreError("nc_adam_step: float32 tensors on a HIP device")
+        if t.shape != param.shape or t.stride() != param.stride():
+            raise L.NiceCoreError("nc_adam_step: param, grad and moments must share shape and strides")
+    if not _dense_layout(param):
+        raise L.NiceCoreError("nc_adam_step: param must be non-overlapping and dense")
+    a = _adam_args(L.NC_ADAM_DENSE, lr, beta1, beta2, eps, weight_decay, step)
+    a.n = param.numel()
+    a.param, a.grad, a.exp_avg, a.exp_avg_sq = (t.data_ptr() for t in ts)
+    stream = torch.cuda.current_stream(param.device).cuda_stream
+    L.check(L.load().nc_adam_step(ctypes.byref(a), stream), "nc_adam_step")
+
+
+class Adam(torch.optim.Optimizer):
+    """``torch.optim.Adam`` drop-in (lr, betas, eps, weight_decay; per-group lr as the
+    Mapper sets it).  amsgrad, maximize and sparse gradients are not supported (the
+    Mapper uses none of them)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False,
+                 maximize=False):
+        if amsgrad or maximize:
+            raise NotImplementedError("nicecore.optim.Adam: amsgrad / maximize")
+        if not (0.0 <= lr and 0.0 <= eps and 0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError(f"invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps}")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                                      maximize=False))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            for p in group["params"]:
+                g = p.grad
+                if g is None:
+                    continue
+                if g.is_sparse:
+                    raise RuntimeError("nicecore.optim.Adam does not support sparse gradients; "
+                                       "use SparseGridAdam with SparseGridGrads")
+                if not _dense_layout(p):
+                    raise L.NiceCoreError("nicecore.optim.Adam: parameters must be non-overlapping and dense")
+                st = self.state[p]
+                if not st:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                if g.stride() != p.stride():  # e.g. a contiguous grad of a channels-last grid
+                    g = torch.empty_like(p, memory_format=torch.preserve_format).copy_(g)
+                st["step"] += 1
+                adam_step_(p, g, st["exp_avg"], st["exp_avg_sq"], lr=group["lr"], beta1=beta1, beta2=beta2,
+                           eps=group["eps"], weight_decay=group["weight_decay"], step=float(st["step"]))
+        return loss
+
+
+class SparseGridAdam:
+    """``torch.optim.SparseAdam``'s rule for the grids of a ``SparseGridGrads``: each
+    ``step()`` updates, per grid, only the voxels in its gradient rows (nc_adam_step,
+    NC_ADAM_SPARSE_ROWS).  Equivalent to torch.optim.SparseAdam over the channels-last
+    row view ``grid.permute(0, 2, 3, 4, 1).reshape(-1, 32)`` with ``sparse.coo(key)`` as
+    its gradient, without materialising either."""
+
+    def __init__(self, grids: dict, sparse, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        self.sparse = sparse
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.grids, self.state = {}, {}
+        for k in sparse.rows:
+            g = grids[k]
+            _, _, _, H, W = g.shape
+            vs = g.stride(4)
+            if g.stride(3) != W * vs or g.stride(2) != H * W * vs or not _dense_layout(g):
+                raise L.NiceCoreError(f"{k}: SparseGridAdam needs a dense grid with voxel index (z*H+y)*W+x")
+            self.grids[k] = g
+            self.state[k] = {"step": 0,
+                             "exp_avg": torch.zeros_like(g, memory_format=torch.preserve_format),
+                             "exp_avg_sq": torch.zeros_like(g, memory_format=torch.preserve_format)}
+
+    @torch.no_grad()
+    def step(self):
+        lib = L.load()
+        beta1, beta2 = self.betas
+        for k, g in self.grids.items():
+            r = self.sparse.rows[k]
+            st = self.state[k]
+            st["step"] += 1
+            a = _adam_args(L.NC_ADAM_SPARSE_ROWS, self.lr, beta1, beta2, self.eps, 0.0, st["step"])
+            a.param, a.grad = g.data_ptr(), r.values.data_ptr()
+            a.exp_avg, a.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+            a.row_voxel, a.row_count, a.row_capacity = r.row_voxel.data_ptr(), r.count.data_ptr(), r.capacity
+            a.voxel_stride, a.channel_stride = g.stride(4), g.stride(1)
+            stream = torch.cuda.current_stream(g.device).cuda_stream
+            L.check(lib.nc_adam_step(ctypes.byref(a), stream), "nc_adam_step")

@@ -118,3 +118,41 @@ def test_sample_args_validated(lib):
     assert b"pre-filter" in lib.nc_last_error()
     assert lib.nc_sample_rays_backward(ctypes.byref(a), None) < 0
     assert b"pose gradient" in lib.nc_last_error()
+
+
+def test_adam_args_validated(lib):
+    """nc_adam_step (ABI v7) rejects bad arguments before any launch."""
+    assert lib.nc_adam_step(None, None) < 0
+    a = L.NcAdamArgs()
+    a.abi_version = L.NC_ABI_VERSION - 1
+    assert lib.nc_adam_step(ctypes.byref(a), None) == -2
+    a.abi_version = L.NC_ABI_VERSION
+    a.lr, a.beta1, a.beta2, a.eps, a.step = 1e-3, 0.9, 0.999, 1e-8, 0.0
+    assert lib.nc_adam_step(ctypes.byref(a), None) < 0
+    assert b"step count" in lib.nc_last_error()
+    a.step, a.beta2 = 1.0, 1.0
+    assert lib.nc_adam_step(ctypes.byref(a), None) < 0
+    assert b"beta" in lib.nc_last_error()
+    a.beta2, a.n = 0.999, 16
+    assert lib.nc_adam_step(ctypes.byref(a), None) < 0
+    assert b"NULL" in lib.nc_last_error()
+    a.mode, a.weight_decay = L.NC_ADAM_SPARSE_ROWS, 0.1
+    assert lib.nc_adam_step(ctypes.byref(a), None) < 0
+    assert b"weight_decay" in lib.nc_last_error()
+    a.mode = 7
+    assert lib.nc_adam_step(ctypes.byref(a), None) < 0
+    assert b"mode" in lib.nc_last_error()
+
+
+def test_adam_optimizer_contract():
+    """nicecore.optim.Adam's constructor: the Mapper's param groups are accepted, the
+    unsupported variants are refused (no silent CPU / torch fallback)."""
+    import torch
+    from nicecore.optim import Adam, _dense_layout
+    p = [torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(2, 3))]
+    opt = Adam([{"params": [p[0]], "lr": 0}, {"params": [p[1]], "lr": 0.1}])
+    assert [g["lr"] for g in opt.param_groups] == [0, 0.1]
+    with pytest.raises(NotImplementedError):
+        Adam(p, amsgrad=True)
+    assert _dense_layout(torch.zeros(1, 32, 3, 4, 5).contiguous(memory_format=torch.channels_last_3d))
+    assert not _dense_layout(torch.zeros(4, 6)[:, :3])
