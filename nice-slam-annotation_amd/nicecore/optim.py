@@ -146,3 +146,104 @@ class SparseGridAdam:
             a.voxel_stride, a.channel_stride = g.stride(4), g.stride(1)
             stream = torch.cuda.current_stream(g.device).cuda_stream
             L.check(lib.nc_adam_step(ctypes.byref(a), stream), "nc_adam_step")
+
+
+class ShardedSparseGridAdam:
+    """ZeRO-style ``SparseGridAdam`` for grids replicated on every rank (SURVEY.md §8e,
+    C5 on 8 GPUs).  Rank r owns the voxel slab ``[r*V/world, (r+1)*V/world)`` of each
+    grid and keeps the Adam moments for that slab only (1/world of the optimiser
+    state).  ``step()`` replaces ``SparseGridGrads.allreduce`` + ``SparseGridAdam.step``:
+
+    1. ``sparse.merge``: the ascending union of the ranks' touched voxels, identical
+       on every rank (nc_sparse_rows_merge), this rank's partial rows permuted into it;
+    2. reduce-scatter of the union's rows to their owners (the union is sorted, so each
+       owner's rows are one contiguous range; ranges padded to the longest);
+    3. each owner applies SparseAdam's rule to its rows (nc_adam_step, moments
+       addressed inside its slab);
+    4. all-gather of the updated parameter rows, written into every replica.
+
+    Results are bit-identical to the unsharded ``allreduce`` + ``SparseGridAdam`` (the
+    row sums and the elementwise rule are the same).  Grids must be channels-last
+    (``[1, 32, D, H, W]`` with channel stride 1), the layout the core's fast path uses.
+    With gloo the exchange goes through host memory."""
+
+    def __init__(self, grids: dict, sparse, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, group=None):
+        import torch.distributed as dist
+        self.sparse, self.group = sparse, group
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.grids, self.state = {}, {}
+        for k in sparse.rows:
+            g = grids[k]
+            if g.stride(1) != 1 or g.stride(4) != 32 or not _dense_layout(g):
+                raise L.NiceCoreError(f"{k}: ShardedSparseGridAdam needs a channels-last [1,32,D,H,W] grid")
+            V = sparse.rows[k].n_voxels
+            v0, v1 = self.rank * V // self.world, (self.rank + 1) * V // self.world
+            self.grids[k] = g
+            self.state[k] = {"step": 0, "slab": (v0, v1),
+                             "exp_avg": torch.zeros(v1 - v0, 32, device=g.device),
+                             "exp_avg_sq": torch.zeros(v1 - v0, 32, device=g.device)}
+
+    @torch.no_grad()
+    def step(self):
+        import torch.distributed as dist
+        lib = L.load()
+        beta1, beta2 = self.betas
+        world, rank, group = self.world, self.rank, self.group
+        self.sparse.merge(group)
+        host = world > 1 and dist.get_backend(group) == "gloo"
+        for k, g in self.grids.items():
+            r = self.sparse.rows[k]
+            st = self.state[k]
+            st["step"] += 1
+            n = self.sparse.count(k)
+            vox, vals = r.row_voxel[:n], r.values[:n]
+            V = r.n_voxels
+            edges = torch.tensor([i * V // world for i in range(world + 1)], dtype=torch.int64, device=g.device)
+            cut = torch.searchsorted(vox, edges).tolist()
+            sizes = [cut[i + 1] - cut[i] for i in range(world)]
+            maxc = max(max(sizes), 1)
+            # 2. reduce-scatter the rows to their slab owners
+            if world > 1:
+                send = torch.zeros(world, maxc, 32, device=g.device)
+                for i in range(world):
+                    send[i, :sizes[i]] = vals[cut[i]:cut[i + 1]]
+                if host:
+                    sh = send.cpu()
+                    dist.all_reduce(sh, group=group)
+                    mine = sh[rank].to(g.device)
+                else:
+                    mine = torch.empty(maxc, 32, device=g.device)
+                    dist.reduce_scatter_tensor(mine, send.view(world * maxc, 32), group=group)
+            else:
+                mine = vals
+            # 3. SparseAdam rule on the owned rows; moments addressed inside the slab
+            own = sizes[rank]
+            my_vox = vox[cut[rank]:cut[rank + 1]]
+            cnt = torch.tensor([own], dtype=torch.int32, device=g.device)
+            v0 = st["slab"][0]
+            a = _adam_args(L.NC_ADAM_SPARSE_ROWS, self.lr, beta1, beta2, self.eps, 0.0, st["step"])
+            a.param, a.grad = g.data_ptr(), mine.data_ptr()
+            a.exp_avg = st["exp_avg"].data_ptr() - v0 * 32 * 4
+            a.exp_avg_sq = st["exp_avg_sq"].data_ptr() - v0 * 32 * 4
+            a.row_voxel, a.row_count, a.row_capacity = my_vox.data_ptr(), cnt.data_ptr(), own
+            a.voxel_stride, a.channel_stride = 32, 1
+            stream = torch.cuda.current_stream(g.device).cuda_stream
+            L.check(lib.nc_adam_step(ctypes.byref(a), stream), "nc_adam_step")
+            if world == 1:
+                continue
+            # 4. all-gather the updated rows into every replica
+            rows = g.permute(0, 2, 3, 4, 1).reshape(-1, 32)  # a view (channels-last)
+            upd = torch.zeros(maxc, 32, device=g.device)
+            upd[:own] = rows[my_vox]
+            if host:
+                parts = [torch.empty(maxc, 32) for _ in range(world)]
+                dist.all_gather(parts, upd.cpu(), group=group)
+                allu = torch.stack(parts).to(g.device)
+            else:
+                allu = torch.empty(world, maxc, 32, device=g.device)
+                dist.all_gather_into_tensor(allu.view(world * maxc, 32), upd, group=group)
+            for i in range(world):
+                if i != rank and sizes[i]:
+                    rows[vox[cut[i]:cut[i + 1]]] = allu[i, :sizes[i]]

@@ -172,6 +172,28 @@ class SparseGridGrads:
         import torch.distributed as dist
         if not dist.is_initialized() or dist.get_world_size(group) == 1:
             return
+        self.merge(group)
+        host = dist.get_backend(group) == "gloo"
+        for key, r in self.rows.items():
+            n = self.count(key)  # the union's size (identical on every rank)
+            if n:
+                v = r.values[:n]
+                if host:
+                    vh = v.cpu()
+                    dist.all_reduce(vh, group=group)
+                    v.copy_(vh)
+                else:
+                    dist.all_reduce(v, group=group)
+
+    def merge(self, group=None):
+        """The first half of ``allreduce``: replace every grid's rows by the ascending
+        union of all ranks' touched voxels (identical on every rank), with this rank's
+        partial gradient rows permuted into it (zero where it has none).  The values
+        are not summed (``allreduce`` sums them; ``ShardedSparseGridAdam`` reduce-
+        scatters them instead)."""
+        import torch.distributed as dist
+        if not dist.is_initialized() or dist.get_world_size(group) == 1:
+            return
         world = dist.get_world_size(group)
         host = dist.get_backend(group) == "gloo"
         lib = L.load()
@@ -210,12 +232,3 @@ class SparseGridGrads:
                     "nc_sparse_rows_merge")
             r.values, r.row_voxel, r.count, r.capacity = new_vals, new_rv, new_cnt, out_cap
             r.claim_bound = out_cap
-            n = self.count(key)  # the union's size (identical on every rank)
-            if n:
-                v = r.values[:n]
-                if host:
-                    vh = v.cpu()
-                    dist.all_reduce(vh, group=group)
-                    v.copy_(vh)
-                else:
-                    dist.all_reduce(v, group=group)

@@ -209,3 +209,24 @@ def test_mapper_iteration_step():
     torch.cuda.synchronize()
     for a, b in zip(dec + grids, clones):
         assert _ulps(a, b) <= ADAM_ULPS
+
+
+@pytest.mark.gpu
+def test_sharded_sparse_adam_two_gloo_ranks(tmp_path):
+    """ZeRO-style ShardedSparseGridAdam over two gloo ranks on one GPU
+    (subprocesses, tests/zero_adam_worker.py): bit-identical to the unsharded
+    allreduce + SparseGridAdam on every rank, and the replicas agree."""
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29637", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "zero_adam_worker.py"), str(tmp_path)],
+                              env=dict(env, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r))) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=110) == 0
+    outs = [torch.load(tmp_path / f"zero_rank{r}.pt", weights_only=True) for r in range(2)]
+    assert set(outs[0]) == set(outs[1])
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    assert outs[0]["grid_fine/1/idx"].numel() > 0
