@@ -199,6 +199,37 @@ def render_batch_ray(grids, prm, dec_bounds, bound, rays_d, rays_o, stage, gt_de
     return depth, var, color
 
 
+def get_rays(H, W, fx, fy, cx, cy, c2w):
+    """common.py:259-277 get_rays: one ray per pixel, pixel centres at integer
+    coordinates, camera looking down -z; c2w [4,4] float32."""
+    i, j = torch.meshgrid(torch.linspace(0, W - 1, W), torch.linspace(0, H - 1, H), indexing="ij")
+    i, j = i.t(), j.t()
+    dirs = torch.stack([(i - cx) / fx, -(j - cy) / fy, -torch.ones_like(i)], -1).reshape(H, W, 1, 3)
+    rays_d = torch.sum(dirs * c2w[:3, :3], -1)
+    rays_o = c2w[:3, -1].expand(rays_d.shape)
+    return rays_o, rays_d
+
+
+def render_img(grids, prm, dec_bounds, bound, H, W, fx, fy, cx, cy, c2w, stage, gt_depth=None,
+               ray_batch_size=100000):
+    """Renderer.py:264-340 render_img: get_rays, then render_batch_ray over chunks of
+    ray_batch_size rays (each chunk with its own max(gt_depth), as the reference's
+    per-call batch max), depth/uncertainty as float64 [H,W], color [H,W,3].
+    (The reference reshapes gt_depth unconditionally, so gt_depth=None raises there;
+    here it renders without depth.)"""
+    with torch.no_grad():
+        rays_o, rays_d = get_rays(H, W, fx, fy, cx, cy, c2w)
+        rays_o, rays_d = rays_o.reshape(-1, 3), rays_d.reshape(-1, 3)
+        gt = gt_depth.reshape(-1) if gt_depth is not None else None
+        dl, ul, cl = [], [], []
+        for s in range(0, rays_d.shape[0], ray_batch_size):
+            e = s + ray_batch_size
+            d, u, c = render_batch_ray(grids, prm, dec_bounds, bound, rays_d[s:e], rays_o[s:e], stage,
+                                       None if gt is None else gt[s:e])
+            dl.append(d.double()); ul.append(u.double()); cl.append(c)
+        return torch.cat(dl).reshape(H, W), torch.cat(ul).reshape(H, W), torch.cat(cl).reshape(H, W, 3)
+
+
 def mapper_loss(depth, color, gt_depth, gt_color=None, w_color=0.2, color_term=False):
     """Mapper.optimize_map's rendering loss (Mapper.py:603-612, nice=True, occupancy on):
     L1 depth over gt > 0 (float64) plus, in the 'color' stage, w_color times the

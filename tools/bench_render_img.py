@@ -1,0 +1,72 @@
+"""Forward-only reuse of the render core: Renderer.render_img
+(Renderer.py:264-340) of one full Replica room0 frame, 680 x 1200 = 816,000 rays in
+chunks of ray_batch_size = 100,000, stage color with a depth image (S = 48), as the
+Visualizer calls it (Visualizer.py:53-59).  Prints frames/s and rays/s; with
+--cpu-rays N also times the CPU oracle (torch, all host threads) on the first N rays
+of the frame for a per-ray CPU rate.
+
+    python tools/bench_render_img.py [--frames 10] [--cpu-rays 2000]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "nice-slam-annotation_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--scene", default="replica_room0")
+    ap.add_argument("--cpu-rays", type=int, default=0)
+    args = ap.parse_args()
+    import bench
+    ns = argparse.Namespace(scene=args.scene, layout="channels_last", rays=16, mode="tracker",
+                            sparse_grads="off")
+    w = bench.build_workload(ns, 0, "cuda")
+    sc, r = w["sc"], w["renderer"]
+    grids = {k: v.detach() for k, v in w["grids"].items()}
+    model = w["model"]
+    # a camera inside the scene looking along its longest axis, a depth image within the bound
+    c2w = torch.eye(4, dtype=torch.float32)
+    c2w[:3, 3] = ((sc.bound[:, 0] + sc.bound[:, 1]) / 2).float()
+    gen = torch.Generator().manual_seed(0)
+    depth = (torch.rand(sc.H, sc.W, generator=gen) * 2.5 + 0.5)
+    depth[torch.rand(sc.H, sc.W, generator=gen) < 0.05] = 0.0
+    c2w_d, depth_d = c2w.cuda(), depth.cuda()
+    for _ in range(2):
+        r.render_img(grids, model, c2w_d, "cuda", "color", gt_depth=depth_d)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.frames):
+        d, u, c = r.render_img(grids, model, c2w_d, "cuda", "color", gt_depth=depth_d)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / args.frames
+    n = sc.H * sc.W
+    out = {"workload": f"{args.scene} render_img {sc.H}x{sc.W}, stage color, S=48, ray_batch_size "
+                       f"{r.ray_batch_size}", "ms_per_frame": round(dt * 1e3, 3), "frames_per_s": round(1 / dt, 2),
+           "rays_per_s": round(n / dt, 1)}
+    if args.cpu_rays:
+        from oracle import nice_oracle as O
+        torch.set_num_threads(min(os.cpu_count() or 1, 16))
+        params = O.params_from_module(model.cpu())
+        gc = {k: v.cpu().contiguous() for k, v in grids.items()}
+        dec_bounds = {"coarse": sc.bound * 2, "middle": sc.bound, "fine": sc.bound, "color": sc.bound}
+        ro, rd = O.get_rays(sc.H, sc.W, sc.fx, sc.fy, sc.cx, sc.cy, c2w)
+        ro, rd = ro.reshape(-1, 3)[:args.cpu_rays], rd.reshape(-1, 3)[:args.cpu_rays]
+        t = time.perf_counter()
+        with torch.no_grad():
+            O.render_batch_ray(gc, params, dec_bounds, sc.bound, rd, ro, "color", depth.reshape(-1)[:args.cpu_rays])
+        cdt = time.perf_counter() - t
+        out["cpu_oracle_rays_per_s"] = round(args.cpu_rays / cdt, 1)
+        out["cpu_threads"] = torch.get_num_threads()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
