@@ -366,6 +366,24 @@ typedef struct nc_adam_args {
 
 int nc_adam_step(const nc_adam_args* args, void* stream);
 
+/* The dense rule over many parameters in one launch per NC_ADAM_MAX_SEGMENTS
+ * (torch.optim.Adam(fused=True) steps all parameters of the optimiser together):
+ * segment i is (param, grad, exp_avg, exp_avg_sq, n) with its group's lr /
+ * weight_decay and its own step count; betas and eps come from `args` (mode and
+ * the pointer fields of `args` are ignored).  (ABI v7) */
+#define NC_ADAM_MAX_SEGMENTS 24
+typedef struct nc_adam_segment {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;
+  double lr, weight_decay, step;
+} nc_adam_segment;
+
+int nc_adam_step_multi(const nc_adam_args* args, const nc_adam_segment* segments, int32_t n_segments,
+                       void* stream);
+
 int nc_abi_version(void);
 const char* nc_last_error(void);
 
@@ -374,7 +392,7 @@ int64_t nc_param_count(int decoder);
 
 /* sizeof() of the ABI structs, for binding-layout checks:
  * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params, 4 nc_sample_args, 5 nc_frustum_args,
- * 6 nc_sparse_rows, 7 nc_pdf_args, 8 nc_adam_args. */
+ * 6 nc_sparse_rows, 7 nc_pdf_args, 8 nc_adam_args, 9 nc_adam_segment. */
 size_t nc_struct_size(int which);
 
 size_t nc_render_workspace_bytes(const nc_render_args* args);

@@ -574,6 +574,7 @@ size_t nc_struct_size(int which) {
     case 6: return sizeof(nc_sparse_rows);
     case 7: return sizeof(nc_pdf_args);
     case 8: return sizeof(nc_adam_args);
+    case 9: return sizeof(nc_adam_segment);
   }
   return 0;
 }
@@ -792,6 +793,23 @@ int nc_adam_step(const nc_adam_args* a, void* stream) {
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return check_hip(timed(KID_ADAM, s, [&] { return launch_adam(*a, s); }), "k_adam");
+}
+
+int nc_adam_step_multi(const nc_adam_args* a, const nc_adam_segment* segs, int32_t n, void* stream) {
+  if (!a || (n > 0 && !segs)) return fail(-1, "nicecore: args or segments is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (n < 0) return fail(-1, "nicecore: adam: negative segment count");
+  if (!(a->beta1 >= 0.0 && a->beta1 < 1.0 && a->beta2 >= 0.0 && a->beta2 < 1.0 && a->eps >= 0.0))
+    return fail(-1, "nicecore: adam needs 0 <= beta < 1, eps >= 0, lr >= 0");
+  for (int i = 0; i < n; ++i) {
+    const nc_adam_segment& g = segs[i];
+    if (g.n < 0 || !(g.step >= 1.0) || !(g.lr >= 0.0)) return fail(-1, "nicecore: adam segment: bad n, step or lr");
+    if (g.n > 0 && (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq))
+      return fail(-1, "nicecore: adam segment: NULL param, grad or moment");
+  }
+  if (n == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_ADAM, s, [&] { return launch_adam_multi(*a, segs, n, s); }), "k_adam_multi");
 }
 
 static int rows_check(const nc_sparse_rows* r, const char* what) {

@@ -84,6 +84,76 @@ __global__ void __launch_bounds__(256) k_adam_rows(const nc_adam_args a, float n
   a.param[o] = a.param[o] + neg_step_size * (m1 / denom);
 }
 
+// Many parameters per launch: block b belongs to the segment whose [blk_off[i],
+// blk_off[i+1]) holds it; each segment is walked float4-wise (scalar when misaligned).
+struct AdamSegs {
+  nc_adam_segment seg[NC_ADAM_MAX_SEGMENTS];
+  int32_t blk_off[NC_ADAM_MAX_SEGMENTS + 1];
+  int32_t vec[NC_ADAM_MAX_SEGMENTS];
+  int32_t n;
+  double beta1, beta2, eps;
+};
+
+__global__ void __launch_bounds__(256) k_adam_multi(const AdamSegs S) {
+  int i = 0;
+  while (i + 1 < S.n && (int)blockIdx.x >= S.blk_off[i + 1]) ++i;
+  const nc_adam_segment& g = S.seg[i];
+  const float bc1 = 1 - pow(S.beta1, g.step);
+  const float bc2_sqrt = sqrt(1 - pow(S.beta2, g.step));
+  const int64_t nb = S.blk_off[i + 1] - S.blk_off[i];
+  const int64_t stride = nb * blockDim.x;
+  const int64_t t0 = (int64_t)(blockIdx.x - S.blk_off[i]) * blockDim.x + threadIdx.x;
+  const int64_t n4 = S.vec[i] ? g.n / 4 : 0;
+  for (int64_t k = t0; k < n4; k += stride) {
+    float4 p = reinterpret_cast<const float4*>(g.param)[k];
+    const float4 gr = reinterpret_cast<const float4*>(g.grad)[k];
+    float4 m = reinterpret_cast<const float4*>(g.exp_avg)[k];
+    float4 v = reinterpret_cast<const float4*>(g.exp_avg_sq)[k];
+    adam_elem(p.x, gr.x, m.x, v.x, g.lr, S.beta1, S.beta2, g.weight_decay, S.eps, bc1, bc2_sqrt);
+    adam_elem(p.y, gr.y, m.y, v.y, g.lr, S.beta1, S.beta2, g.weight_decay, S.eps, bc1, bc2_sqrt);
+    adam_elem(p.z, gr.z, m.z, v.z, g.lr, S.beta1, S.beta2, g.weight_decay, S.eps, bc1, bc2_sqrt);
+    adam_elem(p.w, gr.w, m.w, v.w, g.lr, S.beta1, S.beta2, g.weight_decay, S.eps, bc1, bc2_sqrt);
+    reinterpret_cast<float4*>(g.param)[k] = p;
+    reinterpret_cast<float4*>(g.exp_avg)[k] = m;
+    reinterpret_cast<float4*>(g.exp_avg_sq)[k] = v;
+  }
+  for (int64_t k = n4 * 4 + t0; k < g.n; k += stride) {
+    float p = g.param[k], m = g.exp_avg[k], v = g.exp_avg_sq[k];
+    adam_elem(p, g.grad[k], m, v, g.lr, S.beta1, S.beta2, g.weight_decay, S.eps, bc1, bc2_sqrt);
+    g.param[k] = p;
+    g.exp_avg[k] = m;
+    g.exp_avg_sq[k] = v;
+  }
+}
+
+int launch_adam_multi(const nc_adam_args& a, const nc_adam_segment* segs, int n, hipStream_t s) {
+  // blocks in proportion to each segment's float4 count, >= 1 each, ~4096 in total
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) total += (segs[i].n + 3) / 4;
+  for (int base = 0; base < n; base += NC_ADAM_MAX_SEGMENTS) {
+    AdamSegs S{};
+    S.n = std::min(n - base, NC_ADAM_MAX_SEGMENTS);
+    S.beta1 = a.beta1;
+    S.beta2 = a.beta2;
+    S.eps = a.eps;
+    int32_t off = 0;
+    for (int i = 0; i < S.n; ++i) {
+      const nc_adam_segment& g = segs[base + i];
+      S.seg[i] = g;
+      S.vec[i] = ((reinterpret_cast<uintptr_t>(g.param) | reinterpret_cast<uintptr_t>(g.grad) |
+                   reinterpret_cast<uintptr_t>(g.exp_avg) | reinterpret_cast<uintptr_t>(g.exp_avg_sq)) & 15) == 0;
+      const int64_t work = (g.n + 3) / 4;
+      const int64_t want = std::min<int64_t>((work + 255) / 256, std::max<int64_t>(1, 4096 * work / std::max<int64_t>(total, 1)));
+      S.blk_off[i] = off;
+      off += (int32_t)std::max<int64_t>(want, 1);
+    }
+    S.blk_off[S.n] = off;
+    hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)off), dim3(256), 0, s, S);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  return 0;
+}
+
 int launch_adam(const nc_adam_args& a, hipStream_t s) {
   if (a.mode == NC_ADAM_DENSE) {
     if (a.n == 0) return 0;

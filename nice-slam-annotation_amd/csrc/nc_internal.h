@@ -93,6 +93,7 @@ int launch_frustum_mask(const nc_frustum_args& a, hipStream_t s);
 int launch_sample_pdf(const nc_pdf_args& a, hipStream_t s);
 // optimiser step (nc_adam.hip)
 int launch_adam(const nc_adam_args& a, hipStream_t s);
+int launch_adam_multi(const nc_adam_args& a, const nc_adam_segment* segs, int n, hipStream_t s);
 // sparse gradient rows (nc_sparse.hip)
 int launch_rows_clear(const nc_sparse_rows& r, hipStream_t s);
 int launch_rows_compact(const MlpCtx& m, hipStream_t s);  // after k_grid_gather's claims

@@ -112,6 +112,11 @@ class NcAdamArgs(ctypes.Structure):
                 ("eps", c_double), ("weight_decay", c_double), ("step", c_double)]
 
 
+class NcAdamSegment(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("n", c_int64), ("lr", c_double), ("weight_decay", c_double), ("step", c_double)]
+
+
 NC_ADAM_DENSE = 0
 NC_ADAM_SPARSE_ROWS = 1
 
@@ -134,6 +139,7 @@ EXPORTS = {
     "nc_frustum_mask": (c_int, [POINTER(NcFrustumArgs), c_void_p]),
     "nc_sample_pdf": (c_int, [POINTER(NcPdfArgs), c_void_p]),
     "nc_adam_step": (c_int, [POINTER(NcAdamArgs), c_void_p]),
+    "nc_adam_step_multi": (c_int, [POINTER(NcAdamArgs), POINTER(NcAdamSegment), c_int32, c_void_p]),
     "nc_sparse_rows_clear": (c_int, [POINTER(NcSparseRows), c_void_p]),
     "nc_sparse_merge_temp_bytes": (c_size_t, [c_int64, c_int64]),
     "nc_sparse_rows_merge": (c_int, [POINTER(NcSparseRows), POINTER(NcSparseRows), c_void_p, c_void_p,

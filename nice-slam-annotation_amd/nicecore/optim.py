@@ -4,8 +4,9 @@
 parameters and feature grids (src/Mapper.py:462-485: one param group per decoder set /
 grid with its own lr, StepLR on top; :625 ``optimizer.step()``).  Its update is the
 arithmetic of ``torch.optim.Adam(fused=True)`` (ATen fused_adam_utils.cuh): one
-``k_adam_dense`` launch per parameter reads param/grad/moments once and writes
-param/moments once (28 B per element, HBM-bound), for grids in either memory format.
+``k_adam_multi`` launch for all parameters (up to 24 per launch) reads param/grad/
+moments once and writes param/moments once (28 B per element, HBM-bound), for grids in
+either memory format.
 State (``step``, ``exp_avg``, ``exp_avg_sq``) and ``state_dict`` follow torch.optim.Adam,
 so schedulers and checkpoints keep working.
 
@@ -85,8 +86,8 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        segs, keep, betas, device = [], [], None, None
         for group in self.param_groups:
-            beta1, beta2 = group["betas"]
             for p in group["params"]:
                 g = p.grad
                 if g is None:
@@ -94,19 +95,37 @@ class Adam(torch.optim.Optimizer):
                 if g.is_sparse:
                     raise RuntimeError("nicecore.optim.Adam does not support sparse gradients; "
                                        "use SparseGridAdam with SparseGridGrads")
-                if not _dense_layout(p):
-                    raise L.NiceCoreError("nicecore.optim.Adam: parameters must be non-overlapping and dense")
+                if p.dtype != torch.float32 or p.device.type != "cuda" or not _dense_layout(p):
+                    raise L.NiceCoreError("nicecore.optim.Adam: float32, non-overlapping and dense parameters "
+                                          "on a HIP device")
+                if betas is None:
+                    betas, eps, device = group["betas"], group["eps"], p.device
+                elif group["betas"] != betas or group["eps"] != eps or p.device != device:
+                    self._flush(segs, betas, eps, device)  # one launch per (betas, eps, device)
+                    segs, keep = [], []
+                    betas, eps, device = group["betas"], group["eps"], p.device
                 st = self.state[p]
                 if not st:
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                if g.stride() != p.stride():  # e.g. a contiguous grad of a channels-last grid
+                if g.stride() != p.stride() or g.dtype != torch.float32:  # e.g. a contiguous grad of a channels-last grid
                     g = torch.empty_like(p, memory_format=torch.preserve_format).copy_(g)
+                    keep.append(g)
                 st["step"] += 1
-                adam_step_(p, g, st["exp_avg"], st["exp_avg_sq"], lr=group["lr"], beta1=beta1, beta2=beta2,
-                           eps=group["eps"], weight_decay=group["weight_decay"], step=float(st["step"]))
+                segs.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                             p.numel(), float(group["lr"]), float(group["weight_decay"]), float(st["step"])))
+        if segs:
+            self._flush(segs, betas, eps, device)
         return loss
+
+    @staticmethod
+    def _flush(segs, betas, eps, device):
+        """All segments in one nc_adam_step_multi call (one launch per 24 parameters)."""
+        arr = (L.NcAdamSegment * len(segs))(*[L.NcAdamSegment(*s) for s in segs])
+        a = _adam_args(L.NC_ADAM_DENSE, 0.0, betas[0], betas[1], eps, 0.0, 1.0)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        L.check(L.load().nc_adam_step_multi(ctypes.byref(a), arr, len(segs), stream), "nc_adam_step_multi")
 
 
 class SparseGridAdam:

@@ -230,3 +230,31 @@ def test_sharded_sparse_adam_two_gloo_ranks(tmp_path):
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
     assert outs[0]["grid_fine/1/idx"].numel() > 0
+
+
+@pytest.mark.gpu
+def test_adam_many_parameters_one_call():
+    """More parameters than one k_adam_multi launch holds (24), mixed sizes including
+    empty and single-element ones, three param groups: still bit-identical to fused Adam."""
+    from nicecore.optim import Adam
+    g = torch.Generator().manual_seed(11)
+    sizes = [int(s) for s in torch.randint(0, 3000, (37,), generator=g)] + [1, 0, 4096 * 64 + 3]
+    ps = [torch.randn(s, generator=g).cuda() for s in sizes]
+
+    def run(cls, **kw):
+        mine = [torch.nn.Parameter(p.clone()) for p in ps]
+        groups = [{"params": mine[:10], "lr": 1e-2}, {"params": mine[10:30], "lr": 0.0},
+                  {"params": mine[30:], "lr": 2e-3, "weight_decay": 1e-2}]
+        opt = cls(groups, **kw)
+        for s in range(3):
+            gg = torch.Generator().manual_seed(50 + s)
+            for p in mine:
+                p.grad = torch.randn(p.shape, generator=gg).cuda()
+            opt.step()
+        torch.cuda.synchronize()
+        return mine, opt
+    got, opt = run(Adam)
+    ref, ropt = run(torch.optim.Adam, fused=True)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+        assert torch.equal(opt.state[a]["exp_avg_sq"], ropt.state[b]["exp_avg_sq"])
