@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--sparse-grads", default="auto", choices=["auto", "on", "off"],
                     help="grid gradients as touched-voxel rows (nicecore.sparse); auto = on for "
                          "grids too large for a dense gradient per iteration (C5)")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="split the backward (render_fn.DeferParamGrads) so the grid-gradient "
+                         "all-reduce overlaps the decoder weight gradients; auto = on for N > 1 "
+                         "(BA mode, dense grid gradients)")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -145,6 +149,11 @@ def make_step(w, args, world, device):
     one = torch.ones((), dtype=torch.float64, device=device)  # d loss / d loss, allocated once
     loss_kw = LOSS_KW[args.mode](args.stage)
 
+    overlap = (w["ba"] and sparse is None and
+               (args.overlap == "on" or (args.overlap == "auto" and world > 1)))
+    from nicecore.render_fn import DeferParamGrads
+    defer = DeferParamGrads() if overlap else None
+
     def pre():
         if world > 1:  # Renderer.py:157/:194 use max(gt_depth) over the whole (sharded) batch
             torch.amax(gt, dim=0, keepdim=True, out=dmax)
@@ -155,11 +164,13 @@ def make_step(w, args, world, device):
             t.grad = None
         if sparse is not None:  # touched-voxel grid gradients: forget last step's rows
             sparse.zero_grad()
+        if defer is not None:
+            defer.clear()
         # render_batch_ray + the caller's loss in the same launches (k_loss):
         # Mapper.py:603-612 (BA mode) / Tracker.py:117-131 (tracker mode)
         depth, unc, color, loss = renderer.render_batch_loss(
             grids, model, rd, ro, device, args.stage, gt, gtc, **loss_kw, depth_max=dmax,
-            sparse_grads=sparse)
+            sparse_grads=sparse, defer_param_grads=defer)
         loss.backward(one)  # = loss.backward(), without a fill kernel per step
         return loss
 
@@ -169,21 +180,43 @@ def make_step(w, args, world, device):
             if sparse is not None:  # union of the ranks' touched voxels, then one SUM per grid
                 sparse.allreduce()
 
+    def tail():  # the decoder weight gradients the split backward left out
+        defer.run()
+
+    def split_post(run_tail):
+        # grid gradients are final: start their all-reduce, compute the weight
+        # gradients meanwhile, then reduce those (small) once they exist
+        finish = ND.allreduce_grads_async(gvals) if world > 1 else (lambda: None)
+        run_tail()
+        finish()
+        if world > 1:
+            ND.allreduce_grads(params)
+
     def eager():
         pre()
         body()
-        post()
+        if defer is None:
+            post()
+        else:
+            split_post(tail)
 
     graphed = None
     if not args.eager:
         from nicecore.graph import GraphedStep
         pre()
         g = GraphedStep(body)
+        if defer is None:
+            def graphed():
+                pre()
+                g()
+                post()
+        else:  # two captures: render + loss + backward without dW, then dW + reduction
+            g2 = GraphedStep(tail)
 
-        def graphed():
-            pre()
-            g()
-            post()
+            def graphed():
+                pre()
+                g()
+                split_post(g2)
     return eager, graphed
 
 
@@ -397,7 +430,9 @@ def main():
                                f"{'mapper/BA grads (rays+grids+decoders)' if args.mode == 'ba' else 'tracker grads (rays)'}",
                    "rays_per_gpu": args.rays, "samples_per_ray": S, "stage": args.stage,
                    "mode": args.mode, "grid_layout": args.layout, "parallelism": f"dp{world}",
-                   "grid_grads": "sparse rows" if w["sparse"] is not None else "dense"},
+                   "grid_grads": "sparse rows" if w["sparse"] is not None else "dense",
+                   "overlap": "grid all-reduce beside k_mlp_dw" if (w["ba"] and w["sparse"] is None and (
+                       args.overlap == "on" or (args.overlap == "auto" and world > 1))) else "none"},
         "roofline": roof,
         "launch": "hipGraph replay" if graphed is not None else "eager",
         "eager_ms_per_step": round(eager_ms, 4),

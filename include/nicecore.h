@@ -71,6 +71,11 @@ extern "C" {
  * gradient is 96 multiply-adds per point instead of 8 corner re-reads.  Without it a
  * backward with g_rays_* / g_pts re-reads the corners. */
 #define NC_SAVE_POINT_JACOBIAN 4
+/* nc_render_backward only (ABI v7): stop after the grid and ray gradients; the decoder
+ * weight gradients (k_mlp_dw + slab reduction) are left to nc_render_backward_params,
+ * called later on the same workspace.  Lets a data-parallel caller start the grid-
+ * gradient all-reduce while the weight gradients are still being computed. */
+#define NC_DEFER_PARAM_GRADS 8
 
 /* nc_render_args.loss: the rendering loss computed by the core (optional) */
 #define NC_LOSS_NONE 0
@@ -400,6 +405,10 @@ int nc_render_forward(const nc_render_args* args, void* workspace, size_t worksp
                       void* stream);
 int nc_render_backward(const nc_render_args* args, void* workspace, size_t workspace_bytes,
                        void* stream);
+/* The decoder weight gradients a backward with NC_DEFER_PARAM_GRADS left out: same args
+ * (the decoders' grad pointers), same workspace, before the next forward on it. (ABI v7) */
+int nc_render_backward_params(const nc_render_args* args, void* workspace, size_t workspace_bytes,
+                              void* stream);
 
 /* Kernel timing with HIP events recorded on the launch stream around every
  * launch of the kernels in `kernel_mask` (bit i = kernel id i, see

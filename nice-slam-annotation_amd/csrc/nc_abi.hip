@@ -382,7 +382,8 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
   S = a->n_strat + a->n_surf + a->n_extra;
   P = a->n_rays * S;
-  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC | NC_SAVE_POINT_JACOBIAN)) return fail(-1, "nicecore: unknown flags");
+  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC | NC_SAVE_POINT_JACOBIAN | NC_DEFER_PARAM_GRADS))
+    return fail(-1, "nicecore: unknown flags");
   if (a->loss < NC_LOSS_NONE || a->loss > NC_LOSS_TRACKER) return fail(-1, "nicecore: unknown loss " + std::to_string(a->loss));
   if (a->loss != NC_LOSS_NONE) {
     if (a->loss_flags & ~(NC_LOSS_COLOR | NC_LOSS_DYNAMIC)) return fail(-1, "nicecore: unknown loss_flags");
@@ -484,13 +485,17 @@ int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s, 
 // decoder backward: dX chains + trilinear backward (k_mlp_dx) -> weight gradients
 // -> slab reduction
 int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s, const DetBufs* det,
-                 const RayCtx* rc = nullptr) {
+                 const RayCtx* rc = nullptr, bool defer_params = false) {
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
   if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs, 1), s); }), "k_mlp_dx")) return e;
   bool any_grid = false;
   for (int j = 0; j < m.n_jobs; ++j) any_grid |= m.jobs[j].need_grid != 0;
   if (m.dfeat && any_grid)
     if (int e = check_hip(timed(KID_DET_SCATTER, s, [&] { return launch_det_scatter(m, *det, s); }), "deterministic grid scatter")) return e;
+  if (defer_params) {  // NC_DEFER_PARAM_GRADS: weight gradients later (nc_render_backward_params)
+    if (!rc) return 0;
+    return check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(*rc, s); }), "k_ray_grads");
+  }
   bool any_dw = false;
   for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;
   if (any_dw)
@@ -651,7 +656,30 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   if (!any) return 0;
   if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
   const DetBufs det = det_bufs(ws, w);
-  return mlp_backward(m, a->dec, P, s, &det, need_coord ? &rc : nullptr);  // (+ ray grads, fused)
+  return mlp_backward(m, a->dec, P, s, &det, need_coord ? &rc : nullptr,  // (+ ray grads, fused)
+                      (a->flags & NC_DEFER_PARAM_GRADS) != 0);
+}
+
+int nc_render_backward_params(const nc_render_args* a, void* ws, size_t ws_bytes, void* stream) {
+  Plan pl;
+  Ws w;
+  int64_t P;
+  int S;
+  if (int e = render_prepare(a, pl, w, P, S)) return e;
+  if (int e = check_models(pl, a->grids, a->dec)) return e;
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_rays == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  RayCtx rc;
+  fill_ray(rc, a, pl, ws, w, P, S);
+  MlpCtx m;
+  fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
+  if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
+  bool any_dw = false;
+  for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;
+  if (!any_dw) return 0;
+  if (int e = check_hip(timed(KID_MLP_DW, s, [&] { return launch_mlp_dw(m, s); }), "k_mlp_dw")) return e;
+  return reduce_params(m, a->dec, s, nullptr);
 }
 
 static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "libnicecore.so")
 NC_ABI_VERSION = 7
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
+NC_DEFER_PARAM_GRADS = 8
 NC_SAVE_POINT_JACOBIAN = 4
 NC_LOSS_NONE, NC_LOSS_MAPPER, NC_LOSS_TRACKER = 0, 1, 2
 NC_LOSS_COLOR, NC_LOSS_DYNAMIC = 1, 2
@@ -128,6 +129,7 @@ EXPORTS = {
     "nc_render_workspace_bytes": (c_size_t, [POINTER(NcRenderArgs)]),
     "nc_render_forward": (c_int, [POINTER(NcRenderArgs), c_void_p, c_size_t, c_void_p]),
     "nc_render_backward": (c_int, [POINTER(NcRenderArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_render_backward_params": (c_int, [POINTER(NcRenderArgs), c_void_p, c_size_t, c_void_p]),
     "nc_timing_start": (c_int, [ctypes.c_uint32]),
     "nc_timing_stop": (c_int, [POINTER(c_double), POINTER(c_int64), c_int]),
     "nc_kernel_name": (ctypes.c_char_p, [c_int]),

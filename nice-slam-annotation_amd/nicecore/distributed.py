@@ -41,22 +41,45 @@ def global_depth_max(gt_depth: torch.Tensor, group=None) -> torch.Tensor:
     return m
 
 
+def _dense(t):
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
 def _shared_bases(grads):
-    """Split grads into (buffers reduced whole, remaining grads): a base tensor whose
-    elements are exactly covered by views in ``grads`` (the render core puts every
-    gradient of one backward call into one buffer: render_fn._alloc_grads) is
-    reduced once instead of per view."""
+    """Split grads into (flat 1-D ranges to reduce, remaining grads).  The render core
+    puts every gradient of one backward call into one buffer (render_fn._alloc_grads:
+    grid gradients first, then the decoder parameters), each gradient a dense view of
+    a contiguous range of it; gradients whose ranges tile a stretch of the buffer
+    without gaps are reduced as that one 1-D range (a single collective, and no
+    channels-last views handed to the backend)."""
     by_base = {}
+    rest = []
     for g in grads:
         b = g._base
-        if b is not None and b.is_contiguous():
-            by_base.setdefault(id(b), (b, []))[1].append(g)
-    whole, covered = [], set()
-    for b, views in by_base.values():
-        if sum(v.numel() for v in views) == b.numel() and all(v.dtype == b.dtype for v in views):
-            whole.append(b)
-            covered.update(id(v) for v in views)
-    return whole, [g for g in grads if id(g) not in covered]
+        if b is not None and b.is_contiguous() and b.dtype == g.dtype and _dense(g):
+            off = g.storage_offset() - b.storage_offset()
+            by_base.setdefault(id(b), (b, []))[1].append((off, off + g.numel(), g))
+        else:
+            rest.append(g)
+    ranges = []
+    for b, spans in by_base.values():
+        spans.sort(key=lambda x: x[0])
+        flat = b.reshape(-1)
+        lo, hi = spans[0][0], spans[0][1]
+        for s0, s1, _ in spans[1:]:
+            if s0 == hi:
+                hi = s1
+            else:
+                ranges.append(flat[lo:hi])
+                lo, hi = s0, s1
+        ranges.append(flat[lo:hi])
+    return ranges, rest
 
 
 def allreduce_grads(tensors, group=None, bucket_bytes: int = 4 << 20):
@@ -66,8 +89,16 @@ def allreduce_grads(tensors, group=None, bucket_bytes: int = 4 << 20):
     buffer per backward call) are reduced with one collective each.  Remaining
     gradients larger than ``bucket_bytes`` are reduced in place (async); the small
     ones are packed into flat buckets, reduced, and unpacked."""
+    allreduce_grads_async(tensors, group, bucket_bytes)()
+
+
+def allreduce_grads_async(tensors, group=None, bucket_bytes: int = 4 << 20):
+    """``allreduce_grads`` with every collective issued asynchronously; returns the
+    function that waits for them (and unpacks the small-gradient buckets).  Work
+    enqueued on the current stream between the two overlaps the exchange (bench.py
+    N > 1: the decoder weight gradients run while the grid gradients are reduced)."""
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):
-        return
+        return lambda: None
     grads = [t.grad for t in tensors if t.grad is not None]
     whole, grads = _shared_bases(grads)
     handles = [dist.all_reduce(b, group=group, async_op=True) for b in whole]
@@ -77,13 +108,19 @@ def allreduce_grads(tensors, group=None, bucket_bytes: int = 4 << 20):
     by_dtype = {}
     for g in small:
         by_dtype.setdefault((g.dtype, g.device), []).append(g)
+    buckets = []
     for _, gs in by_dtype.items():
         flat = torch.cat([g.reshape(-1) for g in gs])
-        dist.all_reduce(flat, group=group)
-        o = 0
-        for g in gs:
-            n = g.numel()
-            g.copy_(flat[o:o + n].view_as(g))
-            o += n
-    for h in handles:
-        h.wait()
+        handles.append(dist.all_reduce(flat, group=group, async_op=True))
+        buckets.append((flat, gs))
+
+    def finish():
+        for h in handles:
+            h.wait()
+        for flat, gs in buckets:
+            o = 0
+            for g in gs:
+                n = g.numel()
+                g.copy_(flat[o:o + n].view_as(g))
+                o += n
+    return finish

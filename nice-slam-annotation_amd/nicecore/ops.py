@@ -83,7 +83,7 @@ _LOSS_KINDS = {"mapper": L.NC_LOSS_MAPPER, "tracker": L.NC_LOSS_TRACKER}
 def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, loss="mapper",
                      target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
                      gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None,
-                     sparse_grads=None, n_importance=0, perturb=0.):
+                     sparse_grads=None, n_importance=0, perturb=0., defer_param_grads=None):
     """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
     color, loss) with ``loss`` a float64 device scalar that backpropagates into the
     grids / decoders / rays like the reference's loss expression:
@@ -98,7 +98,8 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
     ``color_term`` adds the colour term (Mapper: stage == 'color' or not nice; Tracker:
     use_color_in_tracking).  ``gt_depth`` is the depth that guides the surface samples;
     by default the target itself (the tracker and the non-coarse mapper); the coarse
-    mapper renders with None."""
+    mapper renders with None.  ``defer_param_grads``: a render_fn.DeferParamGrads that
+    takes the decoder weight gradients out of ``backward()`` (data-parallel overlap)."""
     if loss not in _LOSS_KINDS:
         raise L.NiceCoreError(f"loss must be one of {sorted(_LOSS_KINDS)}")
     if handle_dynamic and loss != "tracker":
@@ -116,7 +117,8 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
             "deterministic": deterministic, "sparse": sparse_grads,
-            "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth, target_color if color_term else None)}
+            "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth, target_color if color_term else None),
+            "defer": defer_param_grads}
     if n_importance > 0:
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
                                              depth_max, n_importance, det=(perturb == 0.))

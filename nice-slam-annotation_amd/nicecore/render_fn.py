@@ -457,6 +457,7 @@ class NiceRenderFn(torch.autograd.Function):
         a.grad_zero, a.grad_zero_floats = None, 0
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
         ctx.sparse = sparse
+        ctx.defer = spec.get("defer")
         ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt, zx)
         a.z_out, a.weights_out = None, None  # pass-1 outputs: not rewritten by the backward
         ctx.grids = grids
@@ -489,10 +490,54 @@ class NiceRenderFn(torch.autograd.Function):
                                          a, device, prezeroed=ctx.grad_buf, sparse=ctx.sparse)
         ctx.grad_buf = None  # a second backward (retain_graph) gets a fresh, zeroed buffer
         stream = torch.cuda.current_stream(device).cuda_stream
-        L.check(lib.nc_render_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
-                "nc_render_backward")
+        defer = ctx.defer if any(needs_params) else None
+        if defer is not None:
+            a.flags |= L.NC_DEFER_PARAM_GRADS
+        try:
+            L.check(lib.nc_render_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
+                    "nc_render_backward")
+        finally:
+            a.flags &= ~L.NC_DEFER_PARAM_GRADS
         pg = _split_param_grads(plan, flats, needs_params)
+        if defer is not None:  # weight gradients: launched and attached by defer.run()
+            defer._add(L.NcRenderArgs.from_buffer_copy(a), ctx.ws, ctx.nbytes, flats,
+                       [(p, g) for p, g in zip(ctx.keep[5], pg) if g is not None])
+            pg = [None] * len(pg)
         return (None, g_ro if need[1] else None, g_rd if need[2] else None, None, *grid_grads, *pg)
+
+
+class DeferParamGrads:
+    """Split a render backward in two so that a data-parallel caller can start the
+    grid-gradient all-reduce while the decoder weight gradients are still being
+    computed (the grid gradients are final after k_mlp_dx; k_mlp_dw comes after it).
+
+    Pass it as ``defer_param_grads=`` to the render call; ``backward()`` then produces
+    the grid and ray gradients only (NC_DEFER_PARAM_GRADS) and leaves the decoder
+    parameters' ``.grad`` untouched; ``run()`` launches the weight gradients
+    (nc_render_backward_params) of every backward since ``clear()`` and attaches them
+    to the parameters (set when ``.grad`` is None, accumulated otherwise).  Both halves
+    are graph-capturable (two nicecore.graph.GraphedStep captures, bench.py N > 1)."""
+
+    def __init__(self):
+        self.pending = []
+
+    def clear(self):
+        self.pending = []
+
+    def _add(self, args, ws, nbytes, flats, pairs):
+        self.pending.append((args, ws, nbytes, flats, pairs))
+
+    def run(self):
+        lib = L.load()
+        for args, ws, nbytes, _flats, pairs in self.pending:
+            stream = torch.cuda.current_stream(ws.device).cuda_stream
+            L.check(lib.nc_render_backward_params(ctypes.byref(args), ws.data_ptr(), nbytes, stream),
+                    "nc_render_backward_params")
+            for p, g in pairs:
+                if p.grad is None:
+                    p.grad = g
+                elif p.grad.data_ptr() != g.data_ptr():
+                    p.grad.add_(g)
 
 
 class NiceEvalFn(torch.autograd.Function):

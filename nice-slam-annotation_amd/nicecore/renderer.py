@@ -79,7 +79,8 @@ class Renderer(object):
 
     def render_batch_loss(self, c, decoders, rays_d, rays_o, device, stage, gt_depth, gt_color=None,
                           loss='mapper', w_color_loss=0.2, color_term=False, handle_dynamic=False,
-                          render_gt_depth='target', depth_max=None, sparse_grads=None):
+                          render_gt_depth='target', depth_max=None, sparse_grads=None,
+                          defer_param_grads=None):
         """render_batch_ray + the rendering loss (ops.render_rays_loss): returns
         (depth, uncertainty, color, loss).  Mapper.optimize_map:
         ``loss='mapper', color_term=(not nice) or stage == 'color',
@@ -90,7 +91,7 @@ class Renderer(object):
                                 loss, gt_color, w_color_loss, color_term, handle_dynamic,
                                 render_gt_depth, self.N_samples, self.N_surface, depth_max,
                                 sparse_grads=sparse_grads, n_importance=self.N_importance,
-                                perturb=self.perturb)
+                                perturb=self.perturb, defer_param_grads=defer_param_grads)
 
     def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
         """Renderer.py:264-340: chunked full-image render, no grad."""

@@ -157,3 +157,20 @@ def test_allreduce_shared_gradient_buffer():
     np.testing.assert_array_equal(buf, np.arange(40, dtype=np.float32) * 3)   # 1x + 2x
     np.testing.assert_array_equal(dgrad, np.full(5, 3.0, dtype=np.float32))
     np.testing.assert_array_equal(agrad, buf[0:6].reshape(2, 3))
+
+
+def test_shared_buffer_ranges():
+    """Gradients that tile parts of one buffer are reduced as 1-D ranges of it: the
+    grid part and the decoder part of the core's buffer separately (bench.py N > 1
+    reduces them at different times), a gap splits a range, a non-view stays apart."""
+    from nicecore import distributed as ND
+    buf = torch.zeros(64)
+    grid = torch.as_strided(buf, (1, 4, 2, 2, 2), (32, 1, 16, 8, 4), 0)   # channels-last-like, 32 floats
+    p1, p2 = buf[32:40].view(2, 4), buf[40:48]
+    p3 = buf[56:64]
+    other = torch.ones(3)
+    ranges, rest = ND._shared_bases([grid])
+    assert [r.numel() for r in ranges] == [32] and rest == []
+    assert ranges[0].data_ptr() == buf.data_ptr() and ranges[0].dim() == 1
+    ranges, rest = ND._shared_bases([p2, p1, p3, other])
+    assert sorted(r.numel() for r in ranges) == [8, 16] and len(rest) == 1
