@@ -489,8 +489,19 @@ __device__ __forceinline__ void param_reduce_body(const ParamReduceCtx& c, int b
     const int w0 = j == 0 ? c.wg_off[0] : (j == 1 ? c.wg_off[1] : c.wg_off[2]);
     const int w1 = j == 0 ? c.wg_off[1] : (j == 1 ? c.wg_off[2] : c.wg_off[3]);
     const float* src = c.slab + (int64_t)w0 * c.slab_stride + e;
-    for (int w = prt; w < w1 - w0; w += PR_PARTS) {
-      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)w * c.slab_stride);
+    auto row = [&](int w) { return *reinterpret_cast<const float4*>(src + (int64_t)w * c.slab_stride); };
+    const int nw = w1 - w0;
+    int w = prt;
+    // four rows in flight, added in the same order as one at a time (bit-identical sums)
+    for (; w + 3 * PR_PARTS < nw; w += 4 * PR_PARTS) {
+      const float4 v0 = row(w), v1 = row(w + PR_PARTS), v2 = row(w + 2 * PR_PARTS), v3 = row(w + 3 * PR_PARTS);
+      acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
+      acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
+      acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
+      acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
+    }
+    for (; w < nw; w += PR_PARTS) {
+      const float4 v = row(w);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
   }
