@@ -16,7 +16,9 @@ sparse_adam) on the touched voxels only, with the moments kept in the grid's own
 layout.  After ``SparseGridGrads.allreduce`` every rank holds the same union and the
 same summed rows, so replicated grids stay identical.
 
-There is no CPU path: the step needs libnicecore.so and a HIP device.
+There is no CPU path: the step needs libnicecore.so and a HIP device.  The step
+count is a host value (as in torch.optim.Adam without ``capturable``), so ``step()``
+runs outside a captured hipGraph: one launch per 24 parameters after the graph replay.
 """
 from __future__ import annotations
 
