@@ -63,6 +63,9 @@ def parse():
                     help="split the backward (render_fn.DeferParamGrads) so the grid-gradient "
                          "all-reduce overlaps the decoder weight gradients; auto = on for N > 1 "
                          "(BA mode, dense grid gradients)")
+    ap.add_argument("--iteration", action="store_true",
+                    help="also time the whole Mapper iteration with the Adam step (nicecore.optim.Adam, "
+                         "capturable) in the same hipGraph; reported as mapper_iteration_ms")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -200,6 +203,7 @@ def make_step(w, args, world, device):
         else:
             split_post(tail)
 
+    make_step.last_body = body
     graphed = None
     if not args.eager:
         from nicecore.graph import GraphedStep
@@ -336,6 +340,31 @@ class _NullTimer:
         return False
 
 
+def time_mapper_iteration(w, args):
+    """render + loss + backward + Adam step (Mapper.py:590-625) as ONE graph replay:
+    nicecore.optim.Adam(capturable=True) over the grids and decoder parameters."""
+    from nicecore.graph import GraphedStep
+    from nicecore.optim import Adam
+    leaves = [g for g in w["grids"].values() if g.requires_grad] + \
+        [p for p in w["model"].parameters() if p.requires_grad]
+    opt = Adam(leaves, lr=1e-4, capturable=True)
+    body = w["body"]
+
+    def it():
+        loss = body()
+        opt.step()
+        return loss
+    g = GraphedStep(it)
+    for _ in range(args.warmup):
+        g()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g()
+    torch.cuda.synchronize()
+    return round(1e3 * (time.perf_counter() - t0) / args.steps, 4)
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -344,6 +373,7 @@ def main():
     L.load()
     w = build_workload(args, rank, device)
     eager, graphed = make_step(w, args, world, device)
+    w["body"] = getattr(make_step, "last_body", None)
     for _ in range(args.warmup):
         eager()
     torch.cuda.synchronize()
@@ -438,6 +468,8 @@ def main():
         "eager_ms_per_step": round(eager_ms, 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1])},
     }
+    if args.iteration and world == 1 and w["ba"] and w["sparse"] is None:
+        out["mapper_iteration_ms"] = time_mapper_iteration(w, args)
     if world == 1 and rank == 0 and args.cpu_seconds > 0:
         from nicecore import scene as S_
         if S_.grids_bytes(S_.make_scene(args.scene).shapes) > (8 << 30):

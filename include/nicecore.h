@@ -376,7 +376,7 @@ int nc_adam_step(const nc_adam_args* args, void* stream);
  * segment i is (param, grad, exp_avg, exp_avg_sq, n) with its group's lr /
  * weight_decay and its own step count; betas and eps come from `args` (mode and
  * the pointer fields of `args` are ignored).  (ABI v7) */
-#define NC_ADAM_MAX_SEGMENTS 24
+#define NC_ADAM_MAX_SEGMENTS 32
 typedef struct nc_adam_segment {
   float* param;
   const float* grad;
@@ -384,6 +384,9 @@ typedef struct nc_adam_segment {
   float* exp_avg_sq;
   int64_t n;
   double lr, weight_decay, step;
+  float* step_dev;      /* optional: the step count in device memory (float32, as torch's
+                           capturable state): incremented by the call, then used instead of
+                           `step` -- a graph-captured step sees the live count */
 } nc_adam_segment;
 
 int nc_adam_step_multi(const nc_adam_args* args, const nc_adam_segment* segments, int32_t n_segments,

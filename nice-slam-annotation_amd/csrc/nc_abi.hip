@@ -831,7 +831,8 @@ int nc_adam_step_multi(const nc_adam_args* a, const nc_adam_segment* segs, int32
     return fail(-1, "nicecore: adam needs 0 <= beta < 1, eps >= 0, lr >= 0");
   for (int i = 0; i < n; ++i) {
     const nc_adam_segment& g = segs[i];
-    if (g.n < 0 || !(g.step >= 1.0) || !(g.lr >= 0.0)) return fail(-1, "nicecore: adam segment: bad n, step or lr");
+    if (g.n < 0 || !(g.step_dev || g.step >= 1.0) || !(g.lr >= 0.0))
+      return fail(-1, "nicecore: adam segment: bad n, step or lr");
     if (g.n > 0 && (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq))
       return fail(-1, "nicecore: adam segment: NULL param, grad or moment");
   }

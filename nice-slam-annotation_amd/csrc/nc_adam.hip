@@ -98,8 +98,9 @@ __global__ void __launch_bounds__(256) k_adam_multi(const AdamSegs S) {
   int i = 0;
   while (i + 1 < S.n && (int)blockIdx.x >= S.blk_off[i + 1]) ++i;
   const nc_adam_segment& g = S.seg[i];
-  const float bc1 = 1 - pow(S.beta1, g.step);
-  const float bc2_sqrt = sqrt(1 - pow(S.beta2, g.step));
+  const double step = g.step_dev ? (double)*g.step_dev : g.step;
+  const float bc1 = 1 - pow(S.beta1, step);
+  const float bc2_sqrt = sqrt(1 - pow(S.beta2, step));
   const int64_t nb = S.blk_off[i + 1] - S.blk_off[i];
   const int64_t stride = nb * blockDim.x;
   const int64_t t0 = (int64_t)(blockIdx.x - S.blk_off[i]) * blockDim.x + threadIdx.x;
@@ -126,10 +127,30 @@ __global__ void __launch_bounds__(256) k_adam_multi(const AdamSegs S) {
   }
 }
 
+constexpr int ADAM_COUNT_MAX = 256;
+struct AdamCounts {
+  float* step[ADAM_COUNT_MAX];
+  int32_t n;
+};
+__global__ void k_adam_count(const AdamCounts C) {  // device step counts: += 1, one launch per call
+  const int i = threadIdx.x;
+  if (i < C.n) *C.step[i] += 1.f;
+}
+
 int launch_adam_multi(const nc_adam_args& a, const nc_adam_segment* segs, int n, hipStream_t s) {
   // blocks in proportion to each segment's float4 count, >= 1 each, ~4096 in total
   int64_t total = 0;
   for (int i = 0; i < n; ++i) total += (segs[i].n + 3) / 4;
+  // device step counts first (capturable mode): every segment then reads its new count
+  AdamCounts C{};
+  for (int i = 0; i <= n; ++i) {
+    if (C.n == ADAM_COUNT_MAX || (i == n && C.n > 0)) {
+      hipLaunchKernelGGL(k_adam_count, dim3(1), dim3(ADAM_COUNT_MAX), 0, s, C);
+      if (hipError_t e = hipGetLastError()) return (int)e;
+      C.n = 0;
+    }
+    if (i < n && segs[i].step_dev) C.step[C.n++] = segs[i].step_dev;
+  }
   for (int base = 0; base < n; base += NC_ADAM_MAX_SEGMENTS) {
     AdamSegs S{};
     S.n = std::min(n - base, NC_ADAM_MAX_SEGMENTS);

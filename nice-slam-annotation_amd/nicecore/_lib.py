@@ -115,7 +115,8 @@ class NcAdamArgs(ctypes.Structure):
 
 class NcAdamSegment(ctypes.Structure):
     _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
-                ("n", c_int64), ("lr", c_double), ("weight_decay", c_double), ("step", c_double)]
+                ("n", c_int64), ("lr", c_double), ("weight_decay", c_double), ("step", c_double),
+                ("step_dev", c_void_p)]
 
 
 NC_ADAM_DENSE = 0

@@ -4,7 +4,7 @@
 parameters and feature grids (src/Mapper.py:462-485: one param group per decoder set /
 grid with its own lr, StepLR on top; :625 ``optimizer.step()``).  Its update is the
 arithmetic of ``torch.optim.Adam(fused=True)`` (ATen fused_adam_utils.cuh): one
-``k_adam_multi`` launch for all parameters (up to 24 per launch) reads param/grad/
+``k_adam_multi`` launch for all parameters (up to 32 per launch) reads param/grad/
 moments once and writes param/moments once (28 B per element, HBM-bound), for grids in
 either memory format.
 State (``step``, ``exp_avg``, ``exp_avg_sq``) and ``state_dict`` follow torch.optim.Adam,
@@ -16,9 +16,10 @@ sparse_adam) on the touched voxels only, with the moments kept in the grid's own
 layout.  After ``SparseGridGrads.allreduce`` every rank holds the same union and the
 same summed rows, so replicated grids stay identical.
 
-There is no CPU path: the step needs libnicecore.so and a HIP device.  The step
-count is a host value (as in torch.optim.Adam without ``capturable``), so ``step()``
-runs outside a captured hipGraph: one launch per 24 parameters after the graph replay.
+There is no CPU path: the step needs libnicecore.so and a HIP device.  With
+``capturable=True`` the step counts live on the device (as torch's capturable Adam) and
+``step()`` can be captured in the same hipGraph as render + loss + backward, so a whole
+Mapper iteration replays as one graph (the learning rates are then fixed at capture).
 """
 from __future__ import annotations
 
@@ -74,13 +75,13 @@ class Adam(torch.optim.Optimizer):
     Mapper uses none of them)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False,
-                 maximize=False):
+                 maximize=False, capturable=False):
         if amsgrad or maximize:
             raise NotImplementedError("nicecore.optim.Adam: amsgrad / maximize")
         if not (0.0 <= lr and 0.0 <= eps and 0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError(f"invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
-                                      maximize=False))
+                                      maximize=False, capturable=capturable))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -107,23 +108,28 @@ class Adam(torch.optim.Optimizer):
                     segs, keep = [], []
                     betas, eps, device = group["betas"], group["eps"], p.device
                 st = self.state[p]
+                cap = group.get("capturable", False)
                 if not st:
-                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device if cap else "cpu")
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 if g.stride() != p.stride() or g.dtype != torch.float32:  # e.g. a contiguous grad of a channels-last grid
                     g = torch.empty_like(p, memory_format=torch.preserve_format).copy_(g)
                     keep.append(g)
-                st["step"] += 1
+                if cap:  # step count on the device, incremented by the launch: graph-capturable
+                    step, step_dev = 0.0, st["step"].data_ptr()
+                else:
+                    st["step"] += 1
+                    step, step_dev = float(st["step"]), None
                 segs.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                             p.numel(), float(group["lr"]), float(group["weight_decay"]), float(st["step"])))
+                             p.numel(), float(group["lr"]), float(group["weight_decay"]), step, step_dev))
         if segs:
             self._flush(segs, betas, eps, device)
         return loss
 
     @staticmethod
     def _flush(segs, betas, eps, device):
-        """All segments in one nc_adam_step_multi call (one launch per 24 parameters)."""
+        """All segments in one nc_adam_step_multi call (one launch per 32 parameters)."""
         arr = (L.NcAdamSegment * len(segs))(*[L.NcAdamSegment(*s) for s in segs])
         a = _adam_args(L.NC_ADAM_DENSE, 0.0, betas[0], betas[1], eps, 0.0, 1.0)
         stream = torch.cuda.current_stream(device).cuda_stream

@@ -234,7 +234,7 @@ def test_sharded_sparse_adam_two_gloo_ranks(tmp_path):
 
 @pytest.mark.gpu
 def test_adam_many_parameters_one_call():
-    """More parameters than one k_adam_multi launch holds (24), mixed sizes including
+    """More parameters than one k_adam_multi launch holds (32), mixed sizes including
     empty and single-element ones, three param groups: still bit-identical to fused Adam."""
     from nicecore.optim import Adam
     g = torch.Generator().manual_seed(11)
@@ -258,3 +258,59 @@ def test_adam_many_parameters_one_call():
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
         assert torch.equal(opt.state[a]["exp_avg_sq"], ropt.state[b]["exp_avg_sq"])
+
+
+@pytest.mark.gpu
+def test_adam_capturable_matches_torch_fused():
+    """capturable=True: step counts on the device, incremented by the launch; same
+    arithmetic as torch's fused Adam (which also reads a float32 device step)."""
+    from nicecore.optim import Adam
+    ps = _params(5)
+    got, opt = _run(Adam, ps, 4, 1e-2, capturable=True)
+    ref, ropt = _run(torch.optim.Adam, ps, 4, 1e-2, fused=True)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+        assert opt.state[a]["step"].device.type == "cuda" and float(opt.state[a]["step"]) == 4.0
+
+
+@pytest.mark.gpu
+def test_mapper_iteration_in_one_graph():
+    """render + loss + backward + Adam step captured in ONE hipGraph (capturable Adam)
+    and replayed: the same parameters as running the iteration eagerly as many times.
+    Decoder-only gradients (no float atomics on their path): bit-identical."""
+    from nicecore.graph import GraphedStep
+    from nicecore.optim import Adam
+    from test_gpu_loss import _setup as loss_setup
+
+    def make():
+        rec, stage, model, g, ro, rd, r = loss_setup("color_depth", want_rays=False)
+        for v in g.values():
+            v.requires_grad_(False)
+        dec = list(model.color_decoder.parameters())
+        for p in model.parameters():
+            p.requires_grad_(False)
+        for p in dec:
+            p.requires_grad_(True)
+        opt = Adam([{"params": dec, "lr": 5e-3}], capturable=True)
+        gt, gtc = rec["gt_depth"].cuda(), rec["gt_color"].cuda()
+
+        def body():
+            for p in dec:
+                p.grad = None
+            d, u, c, L = r.render_batch_loss(g, model, rd, ro, "cuda", stage, gt, gtc, loss="mapper",
+                                             color_term=True)
+            L.backward()
+            opt.step()
+            return L
+        return dec, body
+
+    dec_e, body_e = make()
+    for _ in range(3 + 4):
+        body_e()
+    dec_g, body_g = make()
+    step = GraphedStep(body_g, warmup=3)  # the warmup runs 3 eager iterations
+    for _ in range(4):
+        step()
+    torch.cuda.synchronize()
+    for a, b in zip(dec_g, dec_e):
+        assert torch.equal(a, b)
