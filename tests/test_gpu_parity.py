@@ -211,3 +211,29 @@ def test_graphed_step_matches_eager():
             assert t.grad is None or float(t.grad.abs().max()) == 0.0
         else:
             assert rel_err(t.grad.cpu(), g0.cpu()) <= 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stage", ["fine", "color"])
+def test_mesher_lattice_chunks_match_oracle(stage):
+    """Mesher.eval_points (Mesher.py:367-429) on a lattice spanning the bound: ragged
+    points_batch_size chunks, lattice faces exactly on the bound (masked to 100)."""
+    from oracle import nice_oracle as O
+    bound, cbound, grids, params = load_scene()
+    axes = [torch.linspace(float(bound[i, 0]), float(bound[i, 1]), 17) for i in range(3)]
+    pts = torch.stack(torch.meshgrid(*axes, indexing="ij"), -1).reshape(-1, 3).contiguous()
+    dec_b = {"coarse": cbound, "middle": bound, "fine": bound, "color": bound}
+    with torch.no_grad():
+        ref = O.eval_points(pts.clone(), grids, params, bound, dec_b, stage)
+    model = build_model(params, bound, cbound, "cuda")
+    g = {k: v.cuda() for k, v in grids.items()}
+    r = make_renderer(bound)
+    r.points_batch_size = 1000  # 4913 points -> four full chunks and a ragged one
+    with torch.no_grad():
+        raw = r.eval_points(pts.cuda(), model, g, stage, "cuda").cpu()
+    masked = ref[:, 3] == 100
+    assert bool(masked.any()) and bool((~masked).any())
+    assert torch.equal(raw[:, 3] == 100, masked)
+    assert rel_err(raw[~masked, 3], ref[~masked, 3]) <= OUT_TOL
+    if stage == "color":
+        assert rel_err(raw[:, :3], ref[:, :3]) <= OUT_TOL
