@@ -54,15 +54,18 @@ class Renderer(object):
         """Renderer.py:36-93: NICE.forward plus the strict in-bound mask; points outside
         the renderer bound get raw[:, 3] = 100."""
         self._check_supported()
-        outs = []
+        # Chunks write into one preallocated output and the bound mask is applied once over
+        # all points (elementwise identical to the per-chunk mask; no per-chunk cat).
         b = self.bound
+        out = torch.empty(p.shape[0], 4, dtype=torch.float32, device=p.device)
+        s = 0
         for pi in torch.split(p, self.points_batch_size):
-            m = ((pi[:, 0] < b[0][1]) & (pi[:, 0] > b[0][0]) & (pi[:, 1] < b[1][1]) &
-                 (pi[:, 1] > b[1][0]) & (pi[:, 2] < b[2][1]) & (pi[:, 2] > b[2][0]))
-            raw = _eval_points(decoders, pi, c, stage)
-            occ = torch.where(m, raw[:, 3], torch.full_like(raw[:, 3], 100.0))
-            outs.append(torch.cat([raw[:, :3], occ[:, None]], dim=1))
-        return torch.cat(outs, dim=0)
+            out[s:s + pi.shape[0]] = _eval_points(decoders, pi, c, stage)
+            s += pi.shape[0]
+        m = ((p[:, 0] < b[0][1]) & (p[:, 0] > b[0][0]) & (p[:, 1] < b[1][1]) &
+             (p[:, 1] > b[1][0]) & (p[:, 2] < b[2][1]) & (p[:, 2] > b[2][0]))
+        out[:, 3].masked_fill_(~m, 100.0)
+        return out
 
     def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None,
                          depth_max=None, sparse_grads=None):
