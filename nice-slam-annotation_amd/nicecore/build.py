@@ -14,6 +14,8 @@ import os
 import shutil
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
@@ -47,17 +49,30 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str | None 
     lib = out or LIB
     if out is None and not force and not needs_build():
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-           "-I", INCLUDE, "-I", CSRC, *extra, "-o", lib + ".tmp",
-           *[os.path.join(CSRC, s) for s in SOURCES]]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
-    if verbose and (r.stdout or r.stderr):
-        print(r.stdout + r.stderr)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
+             "-Wno-unused-function", "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC, *extra]
+    # one hipcc per source in parallel, then one link: the wall time is the slowest file
+    with tempfile.TemporaryDirectory(prefix="nicecore_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+
+        def compile_one(k):
+            cmd = [hipcc(), *flags, "-c", "-o", objs[k], os.path.join(CSRC, SOURCES[k])]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            return subprocess.run(cmd, capture_output=True, text=True)
+
+        jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+        with ThreadPoolExecutor(jobs) as ex:
+            results = list(ex.map(compile_one, range(len(SOURCES))))
+        for src, r in zip(SOURCES, results):
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed on {src}:\n" + r.stdout + r.stderr)
+            if verbose and (r.stdout or r.stderr):
+                print(r.stdout + r.stderr)
+        r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp", *objs],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("hipcc link failed:\n" + r.stdout + r.stderr)
     os.replace(lib + ".tmp", lib)
     return lib
 
