@@ -178,14 +178,14 @@ struct Ws {
 // Split `total` resident workgroups over the jobs in proportion to their per-point
 // cost (decoder MACs), each job at least 1 and at most its `blocks` work items;
 // off[j]..off[j+1] are job j's workgroups of a 1-D grid, off[k > n_jobs] = off[n_jobs].
-void split_wgs(int total, int64_t blocks, const Job* jobs, int n_jobs, int32_t* off) {
+void split_wgs(int total, int64_t blocks, const Job* jobs, int n_jobs, int32_t* off, int (*cost)(int) = decoder_macs) {
   if (total < n_jobs) total = n_jobs;
   int64_t wsum = 0;
-  for (int j = 0; j < n_jobs; ++j) wsum += decoder_macs(jobs[j].kind);
+  for (int j = 0; j < n_jobs; ++j) wsum += cost(jobs[j].kind);
   off[0] = 0;
   int64_t acc = 0;
   for (int j = 0; j < n_jobs; ++j) {
-    acc += decoder_macs(jobs[j].kind);
+    acc += cost(jobs[j].kind);
     int64_t n = (total * acc + wsum / 2) / wsum - off[j];  // rounded cumulative share
     if (n < 1) n = 1;
     if (n > blocks) n = blocks > 0 ? blocks : 1;
@@ -279,7 +279,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   std::memcpy(m.dw_off, w.dw_off, sizeof(m.dw_off));
   {  // k_mlp_fwd split: one wave of resident workgroups, 16-point tiles per wave
     const int64_t per = FWD_THREADS / 64 * 16 * FWD_TILES;
-    split_wgs(cu_count() * mlp_blocks_per_cu(0), (P + per - 1) / per, pl.jobs, pl.n_jobs, m.fwd_off);
+    split_wgs(cu_count() * mlp_blocks_per_cu(0), (P + per - 1) / per, pl.jobs, pl.n_jobs, m.fwd_off, fwd_tile_cost);
   }
   m.save_rec = w.save;
   for (int j = 0; j < pl.n_jobs; ++j) {

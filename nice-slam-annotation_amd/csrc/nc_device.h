@@ -112,6 +112,102 @@ struct Net {
 };
 
 // ---------------------------------------------------------------------------
+// Split-f16 MFMA ("3 x f16"): every decoder GEMM runs on v_mfma_f32_16x16x32_f16,
+// which issues at 16x the rate of the f32-input MFMA on gfx950.  An f32 operand x
+// is split into hi = f16(x) (round toward zero) and lo = f16((x - hi) * 2^11); a
+// product sum is  sum(a_hi b_hi) + 2^-11 (sum(a_hi b_lo') + sum(a_lo' b_hi))  in two
+// f32 accumulators (the a_lo b_lo term, ~2^-22 relative, is dropped).  Measured on
+// MI355X (tools/split16_bench.hip, profiles/r02/split16_numerics_rate.log): max error
+// per sum|ab| 4e-8 .. 8e-8 for operands of magnitude 1e-3 .. 300 at K = 32 .. 640,
+// at or below the exact-f32 MFMA chain's 7e-8 .. 1.3e-7; operands below ~6e-5
+// (f16 subnormal range) lose relative precision (5e-7 .. 1e-6 at 1e-5), which is
+// far below every tolerance here.  |x| >= 65504 would overflow hi: decoder
+// activations are O(1) (xavier weights, sin features, grid features).
+//
+// Operand layout: the 8 registers j of lane-group g that hold a 32-feature block in
+// the C layout (feature feat_of(j, g)) are exactly the B operand's k-slots 8g + j,
+// so a layer's accumulators feed the next layer after a split with no data
+// movement; the weight images store each 32-column block with column feat_of(j, g)
+// at slot 8g + j (hslot), one 128-byte row per matrix row: 16-byte chunk g of the hi
+// plane and chunk g of the lo plane at chunk positions g ^ f(row) and (g + 4) ^ f(row),
+// f(row) = (row >> 1) & 7 -- the XOR swizzle that makes every lane group of a
+// ds_read_b128 (MI355X_MICROARCH.md LDS table: 4 x 16 lanes, 64 banks) touch 16
+// distinct 16-byte bank slots when lane (i, g) reads row i, chunk g.
+// ---------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __fp16 halfx2 __attribute__((ext_vector_type(2)));
+constexpr float SPLIT_SCALE = 2048.f;
+constexpr float SPLIT_INV = 1.f / 2048.f;
+constexpr int HROW = 128;  // bytes per image row: 32 hi + 32 lo halves, chunks swizzled
+
+// byte offset inside a row of chunk g (0..3) of plane p (0 hi, 1 lo)
+__host__ __device__ constexpr int hchunk(int row, int g, int p) { return 16 * ((g + 4 * p) ^ ((row >> 1) & 7)); }
+
+__device__ __forceinline__ floatx4 mfma16(half8 a, half8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// MI355X / ROCm 7.2 hazard: the LAST result register of v_mfma_f32_16x16x32_f16 needs
+// 8 wait states before a VALU reads it (the first one needs 7), but hipcc's hazard
+// recognizer pads 7 for every register -- measured with hand-placed s_nops on
+// every CU (tools/mfma_hazard.hip, profiles/r02/mfma_hazard.log: v_mov of v43 after
+// 7 states reads stale data in 65% of waves, after 8 in none).  In k_mlp_dx the
+// compiler's v_pk_mul of those registers at exactly 7 states gave sporadically wrong
+// point gradients.  Every group of split-f16 MFMAs whose results go to VALU ends
+// with mfma16_drain(): a scheduling fence around an s_nop 7, so the readers sit at
+// least 8 states after the last MFMA whatever the compiler counts for the asm.
+__device__ __forceinline__ void mfma16_drain() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// slot (0..31) of feature f (0..31) inside a 32-column block: inverse of feat_of
+__host__ __device__ constexpr int hslot(int f) { return 8 * ((f >> 2) & 3) + 4 * (f >> 4) + (f & 3); }
+
+// split 8 C-layout values (one 32-feature block of a lane) into f16 hi / scaled lo
+__device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const halfx2 h = __builtin_amdgcn_cvt_pkrtz(x[j], x[j + 1]);
+    const float r0 = (x[j] - (float)h[0]) * SPLIT_SCALE;
+    const float r1 = (x[j + 1] - (float)h[1]) * SPLIT_SCALE;
+    const halfx2 l = __builtin_amdgcn_cvt_pkrtz(r0, r1);
+    hi[j] = (_Float16)h[0];
+    hi[j + 1] = (_Float16)h[1];
+    lo[j] = (_Float16)l[0];
+    lo[j + 1] = (_Float16)l[1];
+  }
+}
+
+// f16 weight images (k_mlp_fwd: forward rows; k_mlp_dx: transposed rows).
+//   f32 part first (floats): biases BL [5][32], BC [NFC][32], output WO [4][32], BO [4],
+//   Fourier B FB [3][96]; then, from byte HB, the matrices of pts_linears 0..4 and
+//   fc_c 0..4, each MROWS(m) rows of HROW bytes.
+//   forward image: row kb*32 + o of matrix L holds W[o][32 kb + feat_of(slot)];
+//   transposed image: row c (packed input column) holds W[feat_of(slot)][c].
+// Both images have the same offsets (a matrix with K packed inputs has K rows).
+template <int KIND>
+struct NetH {
+  using N = Net<KIND>;
+  static constexpr int BL = 0;
+  static constexpr int BC = BL + 5 * HID;
+  static constexpr int WO = BC + N::NFC * HID;
+  static constexpr int BO = WO + 4 * HID;
+  static constexpr int FB = BO + 4;
+  static constexpr int F32_FLOATS = ((FB + (N::XYZ ? 3 * EMBP : 0)) + 3) & ~3;
+  static constexpr int HB = F32_FLOATS * 4;  // byte offset of the f16 matrices
+  __host__ __device__ static constexpr int kin(int L) { return L == 0 ? N::IN0 : L == 3 ? N::IN3 : HID; }
+  __host__ __device__ static constexpr int lin_off(int L) {  // bytes
+    int o = HB;
+    for (int k = 0; k < L; ++k) o += kin(k) * HROW;
+    return o;
+  }
+  __host__ __device__ static constexpr int fc_off(int L) { return lin_off(5) + L * N::CD * HROW; }
+  static constexpr int BYTES = fc_off(N::NFC);
+};
+
+// ---------------------------------------------------------------------------
 // Trilinear corners of F.grid_sample(5-D, bilinear, border, align_corners=True)
 // restated from ATen's CPU grid_sampler_3d (the reference runs it through
 // decoder.py:186): unnormalise ((x+1)/2)*(size-1), clip to [0, size-1], corner

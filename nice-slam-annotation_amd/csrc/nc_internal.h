@@ -187,18 +187,34 @@ int mlp_blocks_per_cu(int which);  // 0 k_mlp_fwd, 1 k_mlp_dx, 2 k_mlp_dw
 int rec_stride(int kind);  // floats per point of a decoder's [forward | backward] record
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s);  // grid = c.fwd_off[n_jobs]
 int decoder_macs(int kind);  // multiply-adds per point of one decoder's forward
+int fwd_tile_cost(int kind);  // relative k_mlp_fwd time per tile (split of its workgroups over the jobs)
 int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s);
 int launch_mlp_dw(const MlpCtx& c, hipStream_t s);
 int launch_grid_gather(const MlpCtx& c, hipStream_t s);
 int rec_feat_offset(int kind);  // float offset of the features inside a point record
 int64_t max_param_count();
 
-constexpr int FWD_TILES = 1;      // 16-point tiles per wave (2: interleaved chains, 248 VGPRs: slower)
-constexpr int FWD_THREADS = 768;  // 12 waves, 192 points per WG iteration; measured best of 512/768/1024
-#ifndef NC_DX_THREADS
-#define NC_DX_THREADS 768
+#ifndef NC_FWD_TILES
+#define NC_FWD_TILES 1
 #endif
-constexpr int DX_THREADS = NC_DX_THREADS;   // 12 waves x 16 points, barrier-free; 3 waves/SIMD at <= 170 VGPRs
+#ifndef NC_FWD_THREADS
+#define NC_FWD_THREADS 768
+#endif
+constexpr int FWD_TILES = NC_FWD_TILES;      // 16-point tiles per wave sharing the weight fragments
+constexpr int FWD_THREADS = NC_FWD_THREADS;  // waves per workgroup x 64
+#ifndef NC_DX_THREADS
+#if defined(NC_MFMA_F32) || defined(NC_DX_F32)
+#define NC_DX_THREADS 768
+#else
+#define NC_DX_THREADS 512
+#endif
+#endif
+// k_mlp_dx: barrier-free waves of 16 points.  The split-f16 chains hold ~245 VGPRs:
+// 8 waves (2 per SIMD) run them spill-free; squeezed into 170 VGPRs (12 waves) the
+// kernel spills 58-216 VGPRs and produced sporadically wrong point gradients on
+// MI355X (profiles/r02/dx_flaky_768.log), so 512 is the default.  The f32 A/B build
+// keeps the round-1 12 waves.
+constexpr int DX_THREADS = NC_DX_THREADS;
 #ifndef NC_DW_THREADS
 #define NC_DW_THREADS 1024
 #endif

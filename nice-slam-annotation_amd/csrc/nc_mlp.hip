@@ -28,6 +28,13 @@
 #include "nc_grid.h"
 #include "nc_internal.h"
 
+// A/B builds: -DNC_MFMA_F32 runs every decoder GEMM on the exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32, the round-1 kernels); NC_FWD_F32 / NC_DX_F32 one kernel only.
+#ifdef NC_MFMA_F32
+#define NC_FWD_F32
+#define NC_DX_F32
+#endif
+
 #ifdef NC_ABL_NO_TRIG  // timing-only ablation: no trig at all
 #define NC_SIN(x) (x)
 #define NC_COS(x) (x)
@@ -133,6 +140,142 @@ __device__ __forceinline__ void load_weights(float* lds, const nc_decoder_params
   ow.store(lds, [](int e) { return e < N::NOUT * HID ? N::WO + e : N::BO + (e - N::NOUT * HID); });
   __syncthreads();
 }
+
+// Split-f16 weight image (NetH, nc_device.h).  TR = false: forward rows (k_mlp_fwd),
+// TR = true: transposed rows (k_mlp_dx).  Same one-round-trip prologue as
+// load_weights: all global loads, zero-fill, barrier, hi/lo half stores, barrier.
+template <int KIND, bool TR>
+__device__ __forceinline__ int hpos(int m, int o, int c, int plane) {  // byte offset of W_m[o][packed c]
+  using H = NetH<KIND>;
+  const int base = m < 5 ? H::lin_off(m) : H::fc_off(m - 5);
+  const int row = TR ? c : (c >> 5) * 32 + o;
+  const int s = TR ? hslot(o) : hslot(c & 31);
+  return base + row * HROW + hchunk(row, s >> 3, plane) + 2 * (s & 7);
+}
+
+template <int KIND, bool TR, int NT>
+__device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_params& P) {
+  using N = Net<KIND>;
+  using H = NetH<KIND>;
+  constexpr int CDW = N::XYZ ? HID * N::CD : 1, CB = N::XYZ ? HID : 1, NB = N::XYZ ? 3 * EMB : 1;
+  SegRegs<HID * N::in_real(0), NT> w0;
+  SegRegs<HID * N::in_real(1), NT> w1;
+  SegRegs<HID * N::in_real(2), NT> w2;
+  SegRegs<HID * N::in_real(3), NT> w3;
+  SegRegs<HID * N::in_real(4), NT> w4;
+  SegRegs<5 * HID, NT> bl;
+  SegRegs<CDW, NT> c0, c1, c2, c3, c4;
+  SegRegs<5 * CB, NT> bc;
+  SegRegs<NB, NT> fb;
+  SegRegs<N::NOUT * HID + N::NOUT, NT> ow;
+  w0.load(P.lin_w[0]); w1.load(P.lin_w[1]); w2.load(P.lin_w[2]); w3.load(P.lin_w[3]); w4.load(P.lin_w[4]);
+#pragma unroll
+  for (int k = 0; k < bl.PER; ++k) {
+    const int e = (int)threadIdx.x + k * NT;
+    const int L = e >> 5;
+    const float* b = L == 0 ? P.lin_b[0] : L == 1 ? P.lin_b[1] : L == 2 ? P.lin_b[2] : L == 3 ? P.lin_b[3] : P.lin_b[4];
+    bl.v[k] = (e < 5 * HID) ? b[e & 31] : 0.f;
+  }
+  if constexpr (N::XYZ) {
+    c0.load(P.fc_w[0]); c1.load(P.fc_w[1]); c2.load(P.fc_w[2]); c3.load(P.fc_w[3]); c4.load(P.fc_w[4]);
+#pragma unroll
+    for (int k = 0; k < bc.PER; ++k) {
+      const int e = (int)threadIdx.x + k * NT;
+      const int L = e >> 5;
+      const float* b = L == 0 ? P.fc_b[0] : L == 1 ? P.fc_b[1] : L == 2 ? P.fc_b[2] : L == 3 ? P.fc_b[3] : P.fc_b[4];
+      bc.v[k] = (e < 5 * HID) ? b[e & 31] : 0.f;
+    }
+    fb.load(P.fourier_B);
+  }
+#pragma unroll
+  for (int k = 0; k < ow.PER; ++k) {
+    const int e = (int)threadIdx.x + k * NT;
+    ow.v[k] = (e < N::NOUT * HID) ? P.out_w[e] : (e < N::NOUT * HID + N::NOUT ? P.out_b[e - N::NOUT * HID] : 0.f);
+  }
+  for (int e = threadIdx.x; e < H::BYTES / 16; e += NT) reinterpret_cast<float4*>(lds)[e] = float4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  float* F = reinterpret_cast<float*>(lds);
+  auto mat = [&](auto& regs, int m, int in, bool lin) {
+#pragma unroll
+    for (int k = 0; k < regs.PER; ++k) {
+      const int e = (int)threadIdx.x + k * NT;
+      if (e < HID * in) {
+        const int o = e / in, c = e - o * in, cp = lin ? N::pack_col(m, c) : c;
+        const float v = regs.v[k];
+        const _Float16 h = (_Float16)v;  // hi / scaled lo halves of one weight
+        *reinterpret_cast<_Float16*>(lds + hpos<KIND, TR>(m, o, cp, 0)) = h;
+        *reinterpret_cast<_Float16*>(lds + hpos<KIND, TR>(m, o, cp, 1)) = (_Float16)((v - (float)h) * SPLIT_SCALE);
+      }
+    }
+  };
+  mat(w0, 0, N::in_real(0), true); mat(w1, 1, N::in_real(1), true); mat(w2, 2, N::in_real(2), true);
+  mat(w3, 3, N::in_real(3), true); mat(w4, 4, N::in_real(4), true);
+  bl.store(F, [](int e) { return H::BL + e; });
+  if constexpr (N::XYZ) {
+    mat(c0, 5, N::CD, false); mat(c1, 6, N::CD, false); mat(c2, 7, N::CD, false);
+    mat(c3, 8, N::CD, false); mat(c4, 9, N::CD, false);
+    bc.store(F, [](int e) { return H::BC + e; });
+    fb.store(F, [](int e) {
+      const int k = e / EMB, m = e - k * EMB;
+      return H::FB + k * EMBP + m;
+    });
+  }
+  ow.store(F, [](int e) { return e < N::NOUT * HID ? H::WO + e : H::BO + (e - N::NOUT * HID); });
+  __syncthreads();
+}
+
+// acc (output rows 16 ob + 4g + r) += M[:, block kb] x, both 16-row output blocks,
+// T tiles sharing the weight fragments (forward image rows kb*32 + o)
+template <int T>
+__device__ __forceinline__ void mac_fwd(const char* M, int kb, const half8 (&xh)[T], const half8 (&xl)[T],
+                                        floatx4 (&hh)[T][2], floatx4 (&mx)[T][2], int i, int g) {
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    const int r = kb * 32 + ob * 16 + i;
+    const char* row = M + r * HROW;
+    const half8 wh = *reinterpret_cast<const half8*>(row + hchunk(r, g, 0));
+    const half8 wl = *reinterpret_cast<const half8*>(row + hchunk(r, g, 1));
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      hh[t][ob] = mfma16(wh, xh[t], hh[t][ob]);
+      mx[t][ob] = mfma16(wh, xl[t], mx[t][ob]);
+      mx[t][ob] = mfma16(wl, xh[t], mx[t][ob]);
+    }
+  }
+}
+
+// d input (input tiles ti0 .. ti0+NT of 16 features) += M^T dz, M a transposed image
+// (row = packed input column): A = rows 16 (ti0 + t) + i, B = the split dz block.
+// One K-block per call, so the three products of a tile go to three fresh
+// accumulators (hh, mx, ml): no MFMA takes another MFMA's result as its C operand.
+template <int NT>
+__device__ __forceinline__ void mac_bwd(const char* M, int ti0, half8 zh, half8 zl, floatx4* hh, floatx4* mx,
+                                        floatx4* ml, int i, int g) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int r = 16 * (ti0 + t) + i;
+    const char* row = M + r * HROW;
+    const half8 wh = *reinterpret_cast<const half8*>(row + hchunk(r, g, 0));
+    const half8 wl = *reinterpret_cast<const half8*>(row + hchunk(r, g, 1));
+    hh[t] = mfma16(wh, zh, zero4());
+    mx[t] = mfma16(wh, zl, zero4());
+    ml[t] = mfma16(wl, zh, zero4());
+  }
+}
+
+// out[t] += M^T dz for input tiles ti0 .. ti0+NT, two tiles at a time
+template <int NT>
+__device__ __forceinline__ void bwd_acc(const char* M, int ti0, half8 zh, half8 zl, floatx4* out, int i, int g) {
+#pragma unroll
+  for (int t = 0; t < NT; t += 2) {
+    floatx4 hh[2], mx[2], ml[2];
+    mac_bwd<2>(M, ti0 + t, zh, zl, hh, mx, ml, i, g);
+    mfma16_drain();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) out[t + k] += hh[k] + (mx[k] + ml[k]) * SPLIT_INV;
+  }
+}
+
 
 // ---------------------------------------------------------------------------
 // MFMA building blocks
@@ -397,6 +540,131 @@ __device__ __forceinline__ void wave_forward(const float* lds, int i, int g, Wav
 }
 
 // ---------------------------------------------------------------------------
+// Per-wave forward of one decoder for T 16-point tiles on split-f16 MFMA (NetH image).
+// Same record contents and output as wave_forward; every nn.Linear is
+// mac_fwd over its 32-column input blocks, each block split once (split8) and
+// shared by both 16-row output blocks and, through the weight fragments, by the
+// T tiles.
+// ---------------------------------------------------------------------------
+template <int KIND>
+struct WaveIn {
+  float c[Net<KIND>::CD / 4];  // grid features (C layout; fine: [fine | middle])
+  float pf[3];                 // p.float()
+};
+
+template <int KIND, int T>
+__device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, const WaveIn<KIND> (&R)[T],
+                                               float (&out)[T][4], float* const (&rec)[T]) {
+  using N = Net<KIND>;
+  using H = NetH<KIND>;
+  constexpr int CB = N::CD / 32;
+  const float* F = reinterpret_cast<const float*>(img);
+  half8 ch[CB][T], cl[CB][T];
+#pragma unroll
+  for (int b = 0; b < CB; ++b)
+#pragma unroll
+    for (int t = 0; t < T; ++t) split8(R[t].c + 8 * b, ch[b][t], cl[b][t]);
+  half8 eh[3][T], el[3][T];  // Fourier features sin(p.float() @ B), XYZ decoders
+  if constexpr (N::XYZ) {
+    const float* B = F + H::FB;
+#pragma unroll
+    for (int kb = 0; kb < 3; ++kb)
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = 32 * kb + feat_of(j, g);
+          const float x = __builtin_fmaf(R[t].pf[2], B[2 * EMBP + m],
+                                         __builtin_fmaf(R[t].pf[1], B[EMBP + m], R[t].pf[0] * B[m]));
+          e[j] = (m < EMB) ? NC_SIN(x) : 0.f;
+        }
+        split8(e, eh[kb][t], el[kb][t]);
+      }
+  }
+  unsigned mlo[T], mhi[T];
+  float h[T][8];
+  half8 xh[T], xl[T];    // split input of the next block (h_L)
+  half8 h2h[T], h2l[T];  // split h_2 (skip input of block 3)
+#pragma unroll
+  for (int t = 0; t < T; ++t) mlo[t] = mhi[t] = 0;
+#pragma unroll
+  for (int L = 0; L < 5; ++L) {
+    floatx4 hh[T][2], mx[T][2];
+#pragma unroll
+    for (int t = 0; t < T; ++t) hh[t][0] = hh[t][1] = mx[t][0] = mx[t][1] = zero4();
+    const char* M = img + H::lin_off(L);
+    if (L == 0) {
+      if constexpr (N::XYZ) {
+#pragma unroll
+        for (int kb = 0; kb < 3; ++kb) mac_fwd<T>(M, kb, eh[kb], el[kb], hh, mx, i, g);
+      } else {
+        mac_fwd<T>(M, 0, ch[0], cl[0], hh, mx, i, g);
+      }
+    } else if (L == 3) {
+      if constexpr (N::XYZ) {
+#pragma unroll
+        for (int kb = 0; kb < 3; ++kb) mac_fwd<T>(M, kb, eh[kb], el[kb], hh, mx, i, g);
+        mac_fwd<T>(M, 3, h2h, h2l, hh, mx, i, g);
+      } else {
+        mac_fwd<T>(M, 0, ch[0], cl[0], hh, mx, i, g);
+        mac_fwd<T>(M, 1, h2h, h2l, hh, mx, i, g);
+      }
+    } else {
+      mac_fwd<T>(M, 0, xh, xl, hh, mx, i, g);
+    }
+    const float* bl = F + H::BL + L * HID;
+    floatx4 fh[T][2], fm[T][2];
+    if constexpr (N::XYZ) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) fh[t][0] = fh[t][1] = fm[t][0] = fm[t][1] = zero4();
+#pragma unroll
+      for (int b = 0; b < CB; ++b) mac_fwd<T>(img + H::fc_off(L), b, ch[b], cl[b], fh, fm, i, g);
+    }
+    const float* bc = F + H::BC + L * HID;
+    mfma16_drain();
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ob = j >> 2, r = j & 3, f = 16 * ob + 4 * g + r;
+        const float z = (hh[t][ob][r] + mx[t][ob][r] * SPLIT_INV) + bl[f];
+        const bool p = z > 0.f;
+        float v = p ? z : 0.f;
+        bits |= (p ? 1u : 0u) << j;
+        if constexpr (N::XYZ) v = (v + bc[f]) + (fh[t][ob][r] + fm[t][ob][r] * SPLIT_INV);
+        h[t][j] = v;
+      }
+      if (L < 4) mlo[t] |= bits << (8 * L);
+      else mhi[t] = bits;
+      if (L < 4) split8(h[t], xh[t], xl[t]);
+      if (L == 2) {
+        h2h[t] = xh[t];
+        h2l[t] = xl[t];
+      }
+      if (rec[t]) store_rows<2>(rec[t] + Rec<KIND>::H + HID * L, h[t], g);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    if (rec[t]) {
+      *reinterpret_cast<uint2*>(rec[t] + Rec<KIND>::M + 2 * g) = uint2{mlo[t], mhi[t]};
+      if (g == 0) *reinterpret_cast<float4*>(rec[t] + Rec<KIND>::PF) = float4{R[t].pf[0], R[t].pf[1], R[t].pf[2], 0.f};
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (o >= (KIND == K_COLOR ? 3 : 1)) { out[t][o] = 0.f; continue; }
+      const float* wo = F + H::WO + o * HID;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = s + wo[feat_of(j, g)] * h[t][j];
+      out[t][o] = sum_groups(s) + F[H::BO + o];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // forward kernel
 // ---------------------------------------------------------------------------
 // Constant-index select: a dynamic index into the by-value kernel-argument block
@@ -409,7 +677,11 @@ template <int KIND>
 __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float* lds, int64_t wg, int64_t nwg) {
   constexpr int T = FWD_TILES;
   constexpr int CQ = Net<KIND>::CD / 16;
+#ifdef NC_FWD_F32
   load_weights<KIND, PADW_FWD, FWD_THREADS>(lds, ctx.dec[KIND]);
+#else
+  load_weights_h<KIND, false, FWD_THREADS>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
+#endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
   const int64_t per = 16 * waves * T;  // points per workgroup iteration
@@ -437,7 +709,11 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     // keep the (loop-invariant) LDS weight reads inside the loop: hoisting all of
     // them out of the persistent loop would need thousands of registers
     asm volatile("" ::: "memory");
+#ifdef NC_FWD_F32
     WaveRegs<KIND> R[T];
+#else
+    WaveIn<KIND> R[T];
+#endif
     float* rec[T];
     int64_t pt[T];
 #pragma unroll
@@ -457,7 +733,11 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     }
     load_inputs(blk + nwg);
     float out[T][4];
+#ifdef NC_FWD_F32
     wave_forward<KIND, T>(lds, i, g, R, out, rec);
+#else
+    wave_forward_h<KIND, T>(reinterpret_cast<const char*>(lds), i, g, R, out, rec);
+#endif
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const int64_t p = pt[t];
@@ -529,8 +809,13 @@ struct PhaseMap {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int cmax_(int a, int b) { return a > b ? a : b; }
 // k_mlp_dx LDS: its weight image, then one grid-scatter slice per wave
+#ifdef NC_DX_F32
 constexpr int DX_SLICE_BASE = cmax_(cmax_(Net<K_COARSE, PADW_BWD>::WEIGHTS, Net<K_MID, PADW_BWD>::WEIGHTS),
                                     cmax_(Net<K_FINE, PADW_BWD>::WEIGHTS, Net<K_COLOR, PADW_BWD>::WEIGHTS));
+#else
+constexpr int DX_SLICE_BASE =
+    cmax_(cmax_(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), cmax_(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4;
+#endif
 static_assert(DX_SLICE_BASE % 4 == 0, "scatter slices are float4-aligned");
 constexpr int DX_LDS_FLOATS = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
 static_assert(DX_LDS_FLOATS * 4 <= 160 * 1024, "dX LDS budget");
@@ -545,7 +830,14 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
   const bool need_grid = job.need_grid != 0;
   const bool need_coord = job.need_coord != 0;
   const bool need_dc = need_grid || need_coord;
+#ifdef NC_DX_F32
   load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
+#else
+  load_weights_h<KIND, true, DX_THREADS>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
+  using H = NetH<KIND>;
+  const char* img = reinterpret_cast<const char*>(lds);
+  const float* F = lds;
+#endif
   float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int64_t ntiles = (ctx.P + 15) / 16;
   for (int64_t t = (int64_t)blockIdx.x * waves + wave; t < ntiles; t += (int64_t)gridDim.x * waves) {
@@ -570,6 +862,7 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
       if (need_dw && g == 0)  // k_mlp_dw reads d out from the record
         *reinterpret_cast<float4*>(drec + RC::DOUT) = float4{dout[0], dout[1], dout[2], 0.f};
     }
+#ifdef NC_DX_F32
     float dh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -613,11 +906,66 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         }
       }
     }
+#else
+    float dh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int o = 0; o < N::NOUT; ++o) s = s + F[H::WO + o * HID + feat_of(j, g)] * dout[o];
+      dh[j] = s;
+    }
+    floatx4 dc[2] = {zero4(), zero4()};
+    floatx4 demb[6] = {zero4(), zero4(), zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int L = 4; L >= 0; --L) {
+      if (need_dw && valid) store_rows<2>(drec + RC::DH + HID * L, dh, g);
+      float dz[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dz[j] = mask_bit(mlo, mhi, L, j) ? dh[j] : 0.f;
+      half8 zh, zl;
+      split8(dz, zh, zl);
+      if constexpr (N::XYZ) {
+        if (need_dc) {  // d features (own 32 channels) += Wc_L^T dh
+          half8 yh, yl;
+          split8(dh, yh, yl);
+          bwd_acc<2>(img + H::fc_off(L), 0, yh, yl, dc, i, g);
+        }
+      }
+      const char* M = img + H::lin_off(L);
+      if (L == 0) {
+        if constexpr (N::XYZ) bwd_acc<6>(M, 0, zh, zl, demb, i, g);
+        else if (need_dc) bwd_acc<2>(M, 0, zh, zl, dc, i, g);
+      } else {
+        floatx4 t2[2] = {zero4(), zero4()};
+        if (L == 3) {
+          if constexpr (N::XYZ) {
+            bwd_acc<6>(M, 0, zh, zl, demb, i, g);
+            bwd_acc<2>(M, 6, zh, zl, t2, i, g);
+          } else {
+            if (need_dc) bwd_acc<2>(M, 0, zh, zl, dc, i, g);
+            bwd_acc<2>(M, 2, zh, zl, t2, i, g);
+          }
+        } else {
+          bwd_acc<2>(M, 0, zh, zl, t2, i, g);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dh[r] = t2[0][r];
+          dh[4 + r] = t2[1][r];
+        }
+      }
+    }
+#endif
     float dpf[3] = {0.f, 0.f, 0.f};
     if constexpr (N::XYZ) {
       // dx = d emb * cos(p.float() @ B), produced 4 features at a time: stored for
       // k_mlp_dw and reduced into d p.float() = B dx without keeping all 24 live
+#ifdef NC_DX_F32
       const float* B = lds + N::FB;
+#else
+      const float* B = F + H::FB;
+#endif
       const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < 6; ++t) {
@@ -1001,9 +1349,14 @@ __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
 // launch wrappers / layout queries
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+#ifdef NC_FWD_F32
 constexpr int FWD_LDS_FLOATS =
     cmax(cmax(Net<K_COARSE, PADW_FWD>::WEIGHTS, Net<K_MID, PADW_FWD>::WEIGHTS),
          cmax(Net<K_FINE, PADW_FWD>::WEIGHTS, Net<K_COLOR, PADW_FWD>::WEIGHTS));
+#else
+constexpr int FWD_LDS_FLOATS =
+    cmax(cmax(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), cmax(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4;
+#endif
 constexpr int DW_LDS_FLOATS = cmax(cmax(DwLayout<K_COARSE>::TOTAL, DwLayout<K_MID>::TOTAL),
                                    cmax(DwLayout<K_FINE>::TOTAL, DwLayout<K_COLOR>::TOTAL));
 static_assert(FWD_LDS_FLOATS * 4 <= 160 * 1024, "weight image LDS budget");
@@ -1071,6 +1424,23 @@ int decoder_macs(int kind) {  // SURVEY.md §8a a10-a11 (MAC per point)
     case K_FINE: return 20599;
     default: return 15575;
   }
+}
+
+// k_mlp_fwd on split-f16 MFMA is no longer MAC-bound: per tile the Fourier
+// features, the operand splits and the record stores cost about the same for the
+// three xyz decoders, the fine decoder's second feature block a little more
+int fwd_tile_cost(int kind) {
+#if defined(NC_FWD_F32)
+  return decoder_macs(kind);
+#elif defined(NC_FWD_COST_MACS)
+  return decoder_macs(kind);
+#else
+  switch (kind) {
+    case K_COARSE: return 40;
+    case K_FINE: return 112;
+    default: return 100;
+  }
+#endif
 }
 
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {

@@ -354,6 +354,14 @@ def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device, prez
     return grid_grads, flats
 
 
+def _zero_grads(grid_grads, flats):
+    for g in grid_grads:
+        if g is not None:
+            g.zero_()
+    for f in flats.values():
+        f.zero_()
+
+
 def _split_param_grads(plan, flats, needs_params):
     out = []
     sl = plan.param_slices()
@@ -489,6 +497,10 @@ class NiceRenderFn(torch.autograd.Function):
         grid_grads, flats = _alloc_grads(lib, plan, needs_params, _dense_needs(need[4:8], ctx.sparse), ctx.grids,
                                          a, device, prezeroed=ctx.grad_buf, sparse=ctx.sparse)
         ctx.grad_buf = None  # a second backward (retain_graph) gets a fresh, zeroed buffer
+        if rays_o.shape[0] == 0:  # empty batch: nothing is launched, every gradient is zero
+            _zero_grads(grid_grads, flats)
+            pg = _split_param_grads(plan, flats, needs_params)
+            return (None, g_ro if need[1] else None, g_rd if need[2] else None, None, *grid_grads, *pg)
         stream = torch.cuda.current_stream(device).cuda_stream
         defer = ctx.defer if any(needs_params) else None
         if defer is not None:
@@ -595,8 +607,11 @@ class NiceEvalFn(torch.autograd.Function):
         grid_grads, flats = _alloc_grads(lib, plan, needs_params, _dense_needs(need[2:6], ctx.sparse), ctx.grids,
                                          a, device, sparse=ctx.sparse)
         stream = torch.cuda.current_stream(device).cuda_stream
-        L.check(lib.nc_points_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
-                "nc_points_backward")
+        if a.n_points == 0:  # no points: nothing is launched, every gradient is zero
+            _zero_grads(grid_grads, flats)
+        else:
+            L.check(lib.nc_points_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
+                    "nc_points_backward")
         pg = _split_param_grads(plan, flats, needs_params)
         gp = g_pts.to(ctx.p_dtype).reshape(ctx.p_shape) if g_pts is not None else None
         return (None, gp, *grid_grads, *pg)

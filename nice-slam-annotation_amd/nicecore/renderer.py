@@ -54,14 +54,20 @@ class Renderer(object):
         """Renderer.py:36-93: NICE.forward plus the strict in-bound mask; points outside
         the renderer bound get raw[:, 3] = 100."""
         self._check_supported()
-        # Chunks write into one preallocated output and the bound mask is applied once over
-        # all points (elementwise identical to the per-chunk mask; no per-chunk cat).
+        # Chunks write into one output allocated from the first chunk's dtype and device
+        # (what the decoders return, as the reference's cat) and the bound mask is applied
+        # once over all points (elementwise identical to the per-chunk mask).
         b = self.bound
-        out = torch.empty(p.shape[0], 4, dtype=torch.float32, device=p.device)
+        out = None
         s = 0
         for pi in torch.split(p, self.points_batch_size):
-            out[s:s + pi.shape[0]] = _eval_points(decoders, pi, c, stage)
+            r = _eval_points(decoders, pi, c, stage)
+            if out is None:
+                out = torch.empty(p.shape[0], 4, dtype=r.dtype, device=r.device)
+            out[s:s + pi.shape[0]] = r
             s += pi.shape[0]
+        if out is None:  # no chunk at all
+            out = torch.empty(0, 4, dtype=torch.float32, device=p.device)
         m = ((p[:, 0] < b[0][1]) & (p[:, 0] > b[0][0]) & (p[:, 1] < b[1][1]) &
              (p[:, 1] > b[1][0]) & (p[:, 2] < b[2][1]) & (p[:, 2] > b[2][0]))
         out[:, 3].masked_fill_(~m, 100.0)

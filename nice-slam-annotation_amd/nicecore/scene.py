@@ -31,6 +31,7 @@ GRID_KEYS = ("grid_coarse", "grid_middle", "grid_fine", "grid_color")
 PRESETS = {
     "replica_room0": dict(
         bound=[[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]],
+        marching_cubes_bound=[[-2.9, 8.9], [-3.2, 5.5], [-3.5, 3.3]],  # room0.yaml:4
         H=680, W=1200, fx=600.0, fy=600.0, cx=599.5, cy=339.5, crop_edge=0),
     "scannet_scene0000": dict(
         bound=[[-2.0, 11.0], [-2.0, 11.5], [-2.0, 5.5]],
@@ -152,6 +153,9 @@ class SceneSpec:
     cx: float
     cy: float
     grid_len: dict = field(default_factory=lambda: dict(DEFAULT_GRID_LEN))
+    # meshing.marching_cubes_bound of the scene's config (Mesher.py:443), else the raw
+    # mapping bound
+    marching_cubes_bound: torch.Tensor | None = None
 
 
 def make_scene(name: str, grid_len: dict | None = None) -> SceneSpec:
@@ -162,8 +166,19 @@ def make_scene(name: str, grid_len: dict | None = None) -> SceneSpec:
     ce = p.get("crop_edge", 0)
     if ce > 0:  # src/NICE_SLAM.py:181-185
         H, W, cx, cy = H - 2 * ce, W - 2 * ce, cx - ce, cy - ce
+    mcb = torch.tensor(p.get("marching_cubes_bound", p["bound"]), dtype=torch.float64)
     return SceneSpec(name, bound, grid_shapes(bound, gl), H, W, p["fx"], p["fy"],
-                     cx, cy, gl)
+                     cx, cy, gl, mcb)
+
+
+def mesher_lattice(mc_bound: torch.Tensor, resolution: int, padding: float = 0.05) -> torch.Tensor:
+    """Mesher.get_grid_uniform (src/utils/Mesher.py:443-472): a resolution^3 lattice
+    over marching_cubes_bound widened by ``padding`` on every side, float32 [R^3, 3] in
+    the reference's np.meshgrid ('xy') order."""
+    b = np.asarray(mc_bound, dtype=np.float64)
+    x, y, z = (np.linspace(b[k][0] - padding, b[k][1] + padding, resolution) for k in range(3))
+    xx, yy, zz = np.meshgrid(x, y, z)
+    return torch.tensor(np.vstack([xx.ravel(), yy.ravel(), zz.ravel()]).T, dtype=torch.float)
 
 
 def _random_rotation(gen: torch.Generator) -> torch.Tensor:

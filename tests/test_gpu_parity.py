@@ -214,14 +214,18 @@ def test_graphed_step_matches_eager():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stage", ["fine", "color"])
-def test_mesher_lattice_chunks_match_oracle(stage):
-    """Mesher.eval_points (Mesher.py:367-429) on a lattice spanning the bound: ragged
-    points_batch_size chunks, lattice faces exactly on the bound (masked to 100)."""
+@pytest.mark.parametrize("stage", ["coarse", "fine", "color"])
+@pytest.mark.parametrize("padding", [0.0, 0.05])
+def test_mesher_lattice_chunks_match_oracle(stage, padding):
+    """Mesher.eval_points (Mesher.py:367-429) on the Mesher.get_grid_uniform lattice
+    (Mesher.py:443-472): padding 0.05 puts points strictly outside the renderer bound
+    (clamped grid lookups, occupancy masked to 100, colour still returned), padding 0
+    puts lattice faces exactly on the bound; ragged points_batch_size chunks; stage
+    'coarse' runs the coarse decoder on its 2x bound.  All four channels are compared."""
+    from nicecore.scene import mesher_lattice
     from oracle import nice_oracle as O
     bound, cbound, grids, params = load_scene()
-    axes = [torch.linspace(float(bound[i, 0]), float(bound[i, 1]), 17) for i in range(3)]
-    pts = torch.stack(torch.meshgrid(*axes, indexing="ij"), -1).reshape(-1, 3).contiguous()
+    pts = mesher_lattice(bound, 17, padding).contiguous()
     dec_b = {"coarse": cbound, "middle": bound, "fine": bound, "color": bound}
     with torch.no_grad():
         ref = O.eval_points(pts.clone(), grids, params, bound, dec_b, stage)
@@ -237,3 +241,17 @@ def test_mesher_lattice_chunks_match_oracle(stage):
     assert rel_err(raw[~masked, 3], ref[~masked, 3]) <= OUT_TOL
     if stage == "color":
         assert rel_err(raw[:, :3], ref[:, :3]) <= OUT_TOL
+    else:  # occupancy stages return zero colour channels (decoder.py:341-356)
+        assert not bool(raw[:, :3].any()) and not bool(ref[:, :3].any())
+
+
+@pytest.mark.gpu
+def test_eval_points_empty():
+    """Renderer.eval_points on zero points returns an empty [0, 4] float32 tensor."""
+    bound, cbound, grids, params = load_scene()
+    model = build_model(params, bound, cbound, "cuda")
+    g = {k: v.cuda() for k, v in grids.items()}
+    r = make_renderer(bound)
+    with torch.no_grad():
+        raw = r.eval_points(torch.empty(0, 3, device="cuda"), model, g, "color", "cuda")
+    assert raw.shape == (0, 4) and raw.dtype == torch.float32 and raw.device.type == "cuda"

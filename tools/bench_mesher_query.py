@@ -1,5 +1,7 @@
 """Forward-only point queries at Mesher scale: Mesher.eval_points
-(Mesher.py:367-429) over a resolution^3 lattice spanning the scene bound, split into
+(Mesher.py:367-429) over the resolution^3 lattice of Mesher.get_grid_uniform
+(Mesher.py:443-472: marching_cubes_bound widened by 0.05 on every side, so the points
+past the renderer bound take the masked path too), split into
 points_batch_size chunks, first at stage 'fine' (occupancy for marching cubes,
 Mesher.py:569-575) and then at stage 'color' (vertex colours, Mesher.py:655-666).
 Runs through nicecore's Renderer.eval_points (same mask rule: out-of-bound occupancy
@@ -35,12 +37,15 @@ def main():
     sc, r, model = w["sc"], w["renderer"], w["model"]
     grids = {k: v.detach() for k, v in w["grids"].items()}
     r.points_batch_size = args.batch
-    b = sc.bound.float()
-    axes = [torch.linspace(float(b[i, 0]), float(b[i, 1]), args.res) for i in range(3)]
-    pts = torch.stack(torch.meshgrid(*axes, indexing="ij"), -1).reshape(-1, 3).contiguous()
+    from nicecore.scene import mesher_lattice
+    pts = mesher_lattice(sc.marching_cubes_bound, args.res)
     pts_d = pts.cuda()
-    out = {"workload": f"{args.scene} Mesher lattice {args.res}^3 = {pts.shape[0]} points, "
-                       f"points_batch_size {args.batch}, forward only"}
+    b = sc.bound
+    inside = ((pts[:, 0] > b[0, 0]) & (pts[:, 0] < b[0, 1]) & (pts[:, 1] > b[1, 0]) & (pts[:, 1] < b[1, 1]) &
+              (pts[:, 2] > b[2, 0]) & (pts[:, 2] < b[2, 1]))
+    out = {"workload": f"{args.scene} Mesher.get_grid_uniform lattice {args.res}^3 = {pts.shape[0]} points "
+                       f"(marching_cubes_bound +- 0.05, {100 * (1 - float(inside.double().mean())):.1f}% outside "
+                       f"the renderer bound), points_batch_size {args.batch}, forward only"}
     with torch.no_grad():
         for stage in ("fine", "color"):
             r.eval_points(pts_d, model, grids, stage, "cuda")
