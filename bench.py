@@ -33,6 +33,13 @@ import torch  # noqa: E402
 
 METRIC = "rendered rays/sec (fwd+bwd), Replica room0 1000 rays×48 samples, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
+F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense f16/bf16 MFMA peak
+# k_mlp_fwd / k_mlp_dx run every decoder GEMM as three f16 MFMAs (hi*hi + hi*lo + lo*hi,
+# f32 accumulate; csrc/nc_device.h), so their matrix peak in algorithmic f32 FLOP/s is a
+# third of the f16 peak; k_mlp_dw still runs the exact-f32 MFMA
+SPLIT16_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
+MFMA_PEAK = {"k_mlp_fwd": SPLIT16_PEAK_TFLOPS, "k_mlp_dx": SPLIT16_PEAK_TFLOPS, "k_mlp_dw": FP32_MFMA_PEAK_TFLOPS,
+             "k_grid_gather": FP32_MFMA_PEAK_TFLOPS}
 HBM_PEAK_GBS = 8000.0
 MAC = {"coarse": 6176, "middle": 15479, "fine": 20599, "color": 15575}  # per point
 TRI_FLOP = 8 * 32 * 2  # one trilinear lookup of 32 channels
@@ -436,17 +443,19 @@ def main():
         gbs = by / (avg_ms * 1e-3) / 1e9
         tr = read_traffic(args)
         traffic = ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes")
-        ridge = FP32_MFMA_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # FLOP per byte
+        mpeak = MFMA_PEAK.get(dominant, FP32_MFMA_PEAK_TFLOPS)
+        ridge = mpeak * 1e12 / (HBM_PEAK_GBS * 1e9)  # FLOP per byte
         hbm_bound = fl / by < ridge
         roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dominant,
                 "achieved": round(gbs if hbm_bound else tflops, 3),
-                "peak": HBM_PEAK_GBS if hbm_bound else FP32_MFMA_PEAK_TFLOPS,
+                "peak": HBM_PEAK_GBS if hbm_bound else mpeak,
                 "unit": "GB/s" if hbm_bound else "TFLOP/s",
-                "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+                "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / mpeak, 4),
                 "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
                 "flop_per_launch": fl, "bytes_per_launch": by,
                 "intensity_flop_per_byte": round(fl / by, 2), "ridge_flop_per_byte": round(ridge, 2),
-                "mfma_tflops": round(tflops, 3), "mfma_frac": round(tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+                "mfma_tflops": round(tflops, 3), "mfma_peak_tflops": round(mpeak, 1),
+                "mfma_frac": round(tflops / mpeak, 4),
                 "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                 "timing": timing_src}
 
@@ -455,6 +464,8 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "gemm": "decoder GEMMs of k_mlp_fwd/k_mlp_dx as split-f16 MFMA (3 x f16, f32 accumulate, error at or "
+                "below the f32 MFMA's: tools/split16_bench.hip); k_mlp_dw exact f32 MFMA; sampling/compositing f64",
         "data": "synthetic",
         "config": {"workload": f"{args.scene} {args.rays} rays x {S} samples per GPU, stage {args.stage}, "
                                f"{'mapper/BA grads (rays+grids+decoders)' if args.mode == 'ba' else 'tracker grads (rays)'}",

@@ -620,7 +620,11 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
+#ifdef NC_ABL_NO_ZERO_FILL  // timing-only ablation: the gradient buffer is not zeroed
+  if (false) {
+#else
   if (a->grad_zero && a->grad_zero_floats > 0) {  // the caller's gradient buffer, zeroed by the gather
+#endif
     if ((reinterpret_cast<uintptr_t>(a->grad_zero) & 15) || (a->grad_zero_floats & 3))
       return fail(-1, "nicecore: grad_zero must be 16-byte aligned and a multiple of 4 floats");
     m.zero_fill = reinterpret_cast<float4*>(a->grad_zero);

@@ -151,9 +151,9 @@ __device__ __forceinline__ floatx4 mfma16(half8 a, half8 b, floatx4 c) {
 // 8 wait states before a VALU reads it (the first one needs 7), but hipcc's hazard
 // recognizer pads 7 for every register -- measured with hand-placed s_nops on
 // every CU (tools/mfma_hazard.hip, profiles/r02/mfma_hazard.log: v_mov of v43 after
-// 7 states reads stale data in 65% of waves, after 8 in none).  In k_mlp_dx the
-// compiler's v_pk_mul of those registers at exactly 7 states gave sporadically wrong
-// point gradients.  Every group of split-f16 MFMAs whose results go to VALU ends
+// 7 states reads stale data in 65% of waves, after 8 in none).  In a split-f16 k_mlp_dx
+// the compiler's v_pk_mul of those registers at exactly 7 states gave sporadically
+// wrong point gradients.  Every group of split-f16 MFMAs whose results go to VALU ends
 // with mfma16_drain(): a scheduling fence around an s_nop 7, so the readers sit at
 // least 8 states after the last MFMA whatever the compiler counts for the asm.
 __device__ __forceinline__ void mfma16_drain() {
@@ -180,13 +180,12 @@ __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
   }
 }
 
-// f16 weight images (k_mlp_fwd: forward rows; k_mlp_dx: transposed rows).
+// f16 weight image of k_mlp_fwd.
 //   f32 part first (floats): biases BL [5][32], BC [NFC][32], output WO [4][32], BO [4],
 //   Fourier B FB [3][96]; then, from byte HB, the matrices of pts_linears 0..4 and
 //   fc_c 0..4, each MROWS(m) rows of HROW bytes.
-//   forward image: row kb*32 + o of matrix L holds W[o][32 kb + feat_of(slot)];
-//   transposed image: row c (packed input column) holds W[feat_of(slot)][c].
-// Both images have the same offsets (a matrix with K packed inputs has K rows).
+//   row kb*32 + o of matrix L holds W[o][32 kb + feat_of(slot)] (a matrix with K packed
+//   inputs has K rows).
 template <int KIND>
 struct NetH {
   using N = Net<KIND>;

@@ -203,18 +203,9 @@ int64_t max_param_count();
 constexpr int FWD_TILES = NC_FWD_TILES;      // 16-point tiles per wave sharing the weight fragments
 constexpr int FWD_THREADS = NC_FWD_THREADS;  // waves per workgroup x 64
 #ifndef NC_DX_THREADS
-#if defined(NC_MFMA_F32) || defined(NC_DX_F32)
 #define NC_DX_THREADS 768
-#else
-#define NC_DX_THREADS 512
 #endif
-#endif
-// k_mlp_dx: barrier-free waves of 16 points.  The split-f16 chains hold ~245 VGPRs:
-// 8 waves (2 per SIMD) run them spill-free; squeezed into 170 VGPRs (12 waves) the
-// kernel spills 58-216 VGPRs and produced sporadically wrong point gradients on
-// MI355X (profiles/r02/dx_flaky_768.log), so 512 is the default.  The f32 A/B build
-// keeps the round-1 12 waves.
-constexpr int DX_THREADS = NC_DX_THREADS;
+constexpr int DX_THREADS = NC_DX_THREADS;   // 12 waves x 16 points, barrier-free; 3 waves/SIMD at <= 170 VGPRs
 #ifndef NC_DW_THREADS
 #define NC_DW_THREADS 1024
 #endif

@@ -28,11 +28,10 @@
 #include "nc_grid.h"
 #include "nc_internal.h"
 
-// A/B builds: -DNC_MFMA_F32 runs every decoder GEMM on the exact-f32 MFMA
-// (v_mfma_f32_16x16x4_f32, the round-1 kernels); NC_FWD_F32 / NC_DX_F32 one kernel only.
+// A/B build: -DNC_MFMA_F32 runs the forward decoder GEMMs on the exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32, the round-1 kernel) instead of split-f16.
 #ifdef NC_MFMA_F32
 #define NC_FWD_F32
-#define NC_DX_F32
 #endif
 
 #ifdef NC_ABL_NO_TRIG  // timing-only ablation: no trig at all
@@ -141,19 +140,18 @@ __device__ __forceinline__ void load_weights(float* lds, const nc_decoder_params
   __syncthreads();
 }
 
-// Split-f16 weight image (NetH, nc_device.h).  TR = false: forward rows (k_mlp_fwd),
-// TR = true: transposed rows (k_mlp_dx).  Same one-round-trip prologue as
+// Split-f16 forward weight image (NetH, nc_device.h).  Same one-round-trip prologue as
 // load_weights: all global loads, zero-fill, barrier, hi/lo half stores, barrier.
-template <int KIND, bool TR>
+template <int KIND>
 __device__ __forceinline__ int hpos(int m, int o, int c, int plane) {  // byte offset of W_m[o][packed c]
   using H = NetH<KIND>;
   const int base = m < 5 ? H::lin_off(m) : H::fc_off(m - 5);
-  const int row = TR ? c : (c >> 5) * 32 + o;
-  const int s = TR ? hslot(o) : hslot(c & 31);
+  const int row = (c >> 5) * 32 + o;
+  const int s = hslot(c & 31);
   return base + row * HROW + hchunk(row, s >> 3, plane) + 2 * (s & 7);
 }
 
-template <int KIND, bool TR, int NT>
+template <int KIND, int NT>
 __device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_params& P) {
   using N = Net<KIND>;
   using H = NetH<KIND>;
@@ -203,8 +201,8 @@ __device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_param
         const int o = e / in, c = e - o * in, cp = lin ? N::pack_col(m, c) : c;
         const float v = regs.v[k];
         const _Float16 h = (_Float16)v;  // hi / scaled lo halves of one weight
-        *reinterpret_cast<_Float16*>(lds + hpos<KIND, TR>(m, o, cp, 0)) = h;
-        *reinterpret_cast<_Float16*>(lds + hpos<KIND, TR>(m, o, cp, 1)) = (_Float16)((v - (float)h) * SPLIT_SCALE);
+        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 0)) = h;
+        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 1)) = (_Float16)((v - (float)h) * SPLIT_SCALE);
       }
     }
   };
@@ -243,39 +241,6 @@ __device__ __forceinline__ void mac_fwd(const char* M, int kb, const half8 (&xh)
     }
   }
 }
-
-// d input (input tiles ti0 .. ti0+NT of 16 features) += M^T dz, M a transposed image
-// (row = packed input column): A = rows 16 (ti0 + t) + i, B = the split dz block.
-// One K-block per call, so the three products of a tile go to three fresh
-// accumulators (hh, mx, ml): no MFMA takes another MFMA's result as its C operand.
-template <int NT>
-__device__ __forceinline__ void mac_bwd(const char* M, int ti0, half8 zh, half8 zl, floatx4* hh, floatx4* mx,
-                                        floatx4* ml, int i, int g) {
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int r = 16 * (ti0 + t) + i;
-    const char* row = M + r * HROW;
-    const half8 wh = *reinterpret_cast<const half8*>(row + hchunk(r, g, 0));
-    const half8 wl = *reinterpret_cast<const half8*>(row + hchunk(r, g, 1));
-    hh[t] = mfma16(wh, zh, zero4());
-    mx[t] = mfma16(wh, zl, zero4());
-    ml[t] = mfma16(wl, zh, zero4());
-  }
-}
-
-// out[t] += M^T dz for input tiles ti0 .. ti0+NT, two tiles at a time
-template <int NT>
-__device__ __forceinline__ void bwd_acc(const char* M, int ti0, half8 zh, half8 zl, floatx4* out, int i, int g) {
-#pragma unroll
-  for (int t = 0; t < NT; t += 2) {
-    floatx4 hh[2], mx[2], ml[2];
-    mac_bwd<2>(M, ti0 + t, zh, zl, hh, mx, ml, i, g);
-    mfma16_drain();
-#pragma unroll
-    for (int k = 0; k < 2; ++k) out[t + k] += hh[k] + (mx[k] + ml[k]) * SPLIT_INV;
-  }
-}
-
 
 // ---------------------------------------------------------------------------
 // MFMA building blocks
@@ -680,7 +645,7 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
 #ifdef NC_FWD_F32
   load_weights<KIND, PADW_FWD, FWD_THREADS>(lds, ctx.dec[KIND]);
 #else
-  load_weights_h<KIND, false, FWD_THREADS>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
+  load_weights_h<KIND, FWD_THREADS>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
 #endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
@@ -809,13 +774,8 @@ struct PhaseMap {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int cmax_(int a, int b) { return a > b ? a : b; }
 // k_mlp_dx LDS: its weight image, then one grid-scatter slice per wave
-#ifdef NC_DX_F32
 constexpr int DX_SLICE_BASE = cmax_(cmax_(Net<K_COARSE, PADW_BWD>::WEIGHTS, Net<K_MID, PADW_BWD>::WEIGHTS),
                                     cmax_(Net<K_FINE, PADW_BWD>::WEIGHTS, Net<K_COLOR, PADW_BWD>::WEIGHTS));
-#else
-constexpr int DX_SLICE_BASE =
-    cmax_(cmax_(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), cmax_(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4;
-#endif
 static_assert(DX_SLICE_BASE % 4 == 0, "scatter slices are float4-aligned");
 constexpr int DX_LDS_FLOATS = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
 static_assert(DX_LDS_FLOATS * 4 <= 160 * 1024, "dX LDS budget");
@@ -830,14 +790,7 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
   const bool need_grid = job.need_grid != 0;
   const bool need_coord = job.need_coord != 0;
   const bool need_dc = need_grid || need_coord;
-#ifdef NC_DX_F32
   load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
-#else
-  load_weights_h<KIND, true, DX_THREADS>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
-  using H = NetH<KIND>;
-  const char* img = reinterpret_cast<const char*>(lds);
-  const float* F = lds;
-#endif
   float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int64_t ntiles = (ctx.P + 15) / 16;
   for (int64_t t = (int64_t)blockIdx.x * waves + wave; t < ntiles; t += (int64_t)gridDim.x * waves) {
@@ -862,7 +815,6 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
       if (need_dw && g == 0)  // k_mlp_dw reads d out from the record
         *reinterpret_cast<float4*>(drec + RC::DOUT) = float4{dout[0], dout[1], dout[2], 0.f};
     }
-#ifdef NC_DX_F32
     float dh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -906,66 +858,11 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         }
       }
     }
-#else
-    float dh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int o = 0; o < N::NOUT; ++o) s = s + F[H::WO + o * HID + feat_of(j, g)] * dout[o];
-      dh[j] = s;
-    }
-    floatx4 dc[2] = {zero4(), zero4()};
-    floatx4 demb[6] = {zero4(), zero4(), zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-    for (int L = 4; L >= 0; --L) {
-      if (need_dw && valid) store_rows<2>(drec + RC::DH + HID * L, dh, g);
-      float dz[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dz[j] = mask_bit(mlo, mhi, L, j) ? dh[j] : 0.f;
-      half8 zh, zl;
-      split8(dz, zh, zl);
-      if constexpr (N::XYZ) {
-        if (need_dc) {  // d features (own 32 channels) += Wc_L^T dh
-          half8 yh, yl;
-          split8(dh, yh, yl);
-          bwd_acc<2>(img + H::fc_off(L), 0, yh, yl, dc, i, g);
-        }
-      }
-      const char* M = img + H::lin_off(L);
-      if (L == 0) {
-        if constexpr (N::XYZ) bwd_acc<6>(M, 0, zh, zl, demb, i, g);
-        else if (need_dc) bwd_acc<2>(M, 0, zh, zl, dc, i, g);
-      } else {
-        floatx4 t2[2] = {zero4(), zero4()};
-        if (L == 3) {
-          if constexpr (N::XYZ) {
-            bwd_acc<6>(M, 0, zh, zl, demb, i, g);
-            bwd_acc<2>(M, 6, zh, zl, t2, i, g);
-          } else {
-            if (need_dc) bwd_acc<2>(M, 0, zh, zl, dc, i, g);
-            bwd_acc<2>(M, 2, zh, zl, t2, i, g);
-          }
-        } else {
-          bwd_acc<2>(M, 0, zh, zl, t2, i, g);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dh[r] = t2[0][r];
-          dh[4 + r] = t2[1][r];
-        }
-      }
-    }
-#endif
     float dpf[3] = {0.f, 0.f, 0.f};
     if constexpr (N::XYZ) {
       // dx = d emb * cos(p.float() @ B), produced 4 features at a time: stored for
       // k_mlp_dw and reduced into d p.float() = B dx without keeping all 24 live
-#ifdef NC_DX_F32
       const float* B = lds + N::FB;
-#else
-      const float* B = F + H::FB;
-#endif
       const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < 6; ++t) {

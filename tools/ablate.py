@@ -24,7 +24,6 @@ VARIANTS = {
     "dx_no_coord": ["-DNC_ABL_DX_NO_COORD"],
     "dx_no_trilinear": ["-DNC_ABL_DX_NO_SCATTER", "-DNC_ABL_DX_NO_COORD"],
     "dx512": ["-DNC_DX_THREADS=512"],
-    "dx768": ["-DNC_DX_THREADS=768"],
     "no_sort": ["-DNC_ABL_NO_SORT"],
     "dw512_16": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=16"],
     "dw256_16": ["-DNC_DW_THREADS=256", "-DNC_DW_NPTS=16"],
@@ -36,7 +35,7 @@ VARIANTS = {
     "dw_no_load": ["-DNC_ABL_DW_NO_LOAD"],
     "dw_no_mfma": ["-DNC_ABL_DW_NO_MFMA"],
     "mfma_f32": ["-DNC_MFMA_F32"],
-    "dx_f32": ["-DNC_DX_F32"],
+    "no_zero_fill": ["-DNC_ABL_NO_ZERO_FILL"],
     "dx512": ["-DNC_DX_THREADS=512"],
     "fwd_t2_512": ["-DNC_FWD_TILES=2", "-DNC_FWD_THREADS=512"],
     "fwd_t1_1024": ["-DNC_FWD_THREADS=1024"],
