@@ -36,7 +36,6 @@ VARIANTS = {
     "dw_no_mfma": ["-DNC_ABL_DW_NO_MFMA"],
     "mfma_f32": ["-DNC_MFMA_F32"],
     "no_zero_fill": ["-DNC_ABL_NO_ZERO_FILL"],
-    "dx512": ["-DNC_DX_THREADS=512"],
     "fwd_t2_512": ["-DNC_FWD_TILES=2", "-DNC_FWD_THREADS=512"],
     "fwd_t1_1024": ["-DNC_FWD_THREADS=1024"],
     "fwd_t2_768": ["-DNC_FWD_TILES=2"],
