@@ -34,11 +34,11 @@ import torch  # noqa: E402
 METRIC = "rendered rays/sec (fwd+bwd), Replica room0 1000 rays×48 samples, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense f16/bf16 MFMA peak
-# k_mlp_fwd / k_mlp_dx run every decoder GEMM as three f16 MFMAs (hi*hi + hi*lo + lo*hi,
-# f32 accumulate; csrc/nc_device.h), so their matrix peak in algorithmic f32 FLOP/s is a
-# third of the f16 peak; k_mlp_dw still runs the exact-f32 MFMA
+# k_mlp_fwd runs every decoder GEMM as three f16 MFMAs (hi*hi + hi*lo + lo*hi, f32
+# accumulate; csrc/nc_device.h), so its matrix peak in algorithmic f32 FLOP/s is a third of
+# the f16 peak; k_mlp_dx and k_mlp_dw run the exact-f32 MFMA
 SPLIT16_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
-MFMA_PEAK = {"k_mlp_fwd": SPLIT16_PEAK_TFLOPS, "k_mlp_dx": SPLIT16_PEAK_TFLOPS, "k_mlp_dw": FP32_MFMA_PEAK_TFLOPS,
+MFMA_PEAK = {"k_mlp_fwd": SPLIT16_PEAK_TFLOPS, "k_mlp_dx": FP32_MFMA_PEAK_TFLOPS, "k_mlp_dw": FP32_MFMA_PEAK_TFLOPS,
              "k_grid_gather": FP32_MFMA_PEAK_TFLOPS}
 HBM_PEAK_GBS = 8000.0
 MAC = {"coarse": 6176, "middle": 15479, "fine": 20599, "color": 15575}  # per point
@@ -326,7 +326,7 @@ def read_traffic(args):
     import glob
     want = {"scene": args.scene, "rays": args.rays, "stage": args.stage, "mode": args.mode,
             "layout": args.layout}
-    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "*traffic*.json")), reverse=True):
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*traffic*.json"), recursive=True), reverse=True):
         try:
             with open(fn) as f:
                 d = json.load(f)
@@ -464,8 +464,9 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "gemm": "decoder GEMMs of k_mlp_fwd/k_mlp_dx as split-f16 MFMA (3 x f16, f32 accumulate, error at or "
-                "below the f32 MFMA's: tools/split16_bench.hip); k_mlp_dw exact f32 MFMA; sampling/compositing f64",
+        "gemm": "decoder GEMMs of k_mlp_fwd as split-f16 MFMA (3 x f16, f32 accumulate, error at or "
+                "below the f32 MFMA's: tools/split16_bench.hip); k_mlp_dx/k_mlp_dw exact f32 MFMA; "
+                "sampling/compositing f64",
         "data": "synthetic",
         "config": {"workload": f"{args.scene} {args.rays} rays x {S} samples per GPU, stage {args.stage}, "
                                f"{'mapper/BA grads (rays+grids+decoders)' if args.mode == 'ba' else 'tracker grads (rays)'}",

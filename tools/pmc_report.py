@@ -21,7 +21,7 @@ for k, c in sorted(vals.items()):
     print(f"   wait_any {g('SQ_WAIT_ANY') / wc:.2f}  wait_inst_any {g('SQ_WAIT_INST_ANY') / wc:.2f}  "
           f"active_inst_any {g('SQ_ACTIVE_INST_ANY') / wc:.2f}  wait_inst_lds {g('SQ_WAIT_INST_LDS') / wc:.2f}")
     mf = g("SQ_INSTS_VALU_MFMA_F32")
-    print(f"   insts: valu {g('SQ_INSTS_VALU'):.3g} (per mfma {g('SQ_INSTS_VALU') / max(mf, 1):.2f})  mfma {mf:.3g}  "
+    print(f"   insts: valu {g('SQ_INSTS_VALU'):.3g} (per mfma {g('SQ_INSTS_VALU') / max(mf, 1):.2f})  mfma_f32 {mf:.3g}  "
           f"lds {g('SQ_INSTS_LDS'):.3g} (per mfma {g('SQ_INSTS_LDS') / max(mf, 1):.2f})  salu {g('SQ_INSTS_SALU'):.3g}  vmem {g('SQ_INSTS_VMEM'):.3g}")
     print(f"   mfma_busy/busy {g('SQ_VALU_MFMA_BUSY_CYCLES') / max(g('SQ_BUSY_CYCLES'), 1):.3f}  "
           f"lds_bank_conflict/active_lds {g('SQ_LDS_BANK_CONFLICT') / max(g('SQ_ACTIVE_INST_LDS'), 1):.3f}  "
