@@ -73,6 +73,11 @@ def parse():
     ap.add_argument("--iteration", action="store_true",
                     help="also time the whole Mapper iteration with the Adam step (nicecore.optim.Adam, "
                          "capturable) in the same hipGraph; reported as mapper_iteration_ms")
+    ap.add_argument("--fix-fine", action="store_true",
+                    help="the Mapper's fix_fine=True (configs/nice_slam.yaml:62, Mapper.py:416-424): only "
+                         "the color decoder's parameters require grad, the ones the Mapper optimises. "
+                         "Default: every decoder parameter requires grad, as in the reference, whose "
+                         "autograd computes (and never uses) the middle and fine decoder gradients")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -123,6 +128,10 @@ def build_workload(args, rank, device):
         g.requires_grad_(ba)
     for p in model.parameters():
         p.requires_grad_(ba)
+    if args.fix_fine:  # only the color decoder is in the Mapper's optimizer
+        for n in ("coarse", "middle", "fine"):
+            for p in getattr(model, n + "_decoder").parameters():
+                p.requires_grad_(False)
     sparse = None
     if ba and (args.sparse_grads == "on" or
                (args.sparse_grads == "auto" and S.grids_bytes(sc.shapes) > (2 << 30))):
@@ -231,7 +240,7 @@ def make_step(w, args, world, device):
     return eager, graphed
 
 
-def algorithmic_flops_per_ray(stage, S, mode):
+def algorithmic_flops_per_ray(stage, S, mode, fix_fine=False):
     """Algorithmic FLOP per ray of each decoder kernel:
     k_mlp_fwd = decoder MACs + trilinear lookups, k_mlp_dx = dX-chain MACs,
     k_mlp_dw = weight-gradient MACs (BA mode only)."""
@@ -240,7 +249,7 @@ def algorithmic_flops_per_ray(stage, S, mode):
     lk_fwd = {"coarse": 1, "middle": 1, "fine": 3, "color": 4}[stage]
     fwd = 2 * sum(MAC[d] for d in decs) + TRI_FLOP * lk_fwd
     dx = 2 * sum(MAC_DX[d] for d in decs)
-    dw = 2 * sum(MAC[d] for d in decs) if mode == "ba" else 0
+    dw = 2 * sum(MAC[d] for d in decs if not fix_fine or d == "color") if mode == "ba" else 0
     return {"k_mlp_fwd": fwd * S, "k_mlp_dx": dx * S, "k_mlp_dw": dw * S,
             "k_grid_gather": TRI_FLOP * LOOKUPS_UNIQUE[stage] * S}
 
@@ -258,7 +267,7 @@ FEAT = {"coarse": 32, "middle": 32, "fine": 64, "color": 32}
 NOUT = {"coarse": 1, "middle": 1, "fine": 1, "color": 3}
 
 
-def algorithmic_bytes_per_point(stage, mode, jac=False):
+def algorithmic_bytes_per_point(stage, mode, jac=False, fix_fine=False):
     """HBM bytes a kernel must move per sample point: its inputs and
     outputs, the saved activation records included (they are the backward's input)."""
     decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
@@ -270,9 +279,10 @@ def algorithmic_bytes_per_point(stage, mode, jac=False):
     # NC_SAVE_POINT_JACOBIAN); BA mode adds the backward record out and the grid-gradient
     # scatter, counted as §8(d) does: 2 x 1,024 B (read-modify-write of 8 corner rows)
     ba = mode == "ba"
+    wdw = [d for d in decs if not fix_fine or d == "color"] if ba else []  # decoders with dW
     dx = sum(32 + 4 * NOUT[d] + 16 + 16 + 24 + (384 if jac else 1024) +
-             ((4 * (REC_STRIDE[d] - REC_LEN[d]) + 2 * 1024) if ba else 0) for d in decs)
-    dw = sum(4 * REC_STRIDE[d] for d in decs) if mode == "ba" else 0
+             (2 * 1024 if ba else 0) + (4 * (REC_STRIDE[d] - REC_LEN[d]) if d in wdw else 0) for d in decs)
+    dw = sum(4 * REC_STRIDE[d] for d in wdw)
     # k_grid_gather: 8 corner rows of 128 B per distinct lookup, 128 B of features out per
     # lookup, and the 384-B trilinear Jacobian of each decoder's own lookup (ray gradients)
     gather = 1024 * LOOKUPS_UNIQUE[stage] + 128 * LOOKUPS_FWD[stage] + (384 * len(decs) if jac else 0)
@@ -432,9 +442,9 @@ def main():
     avg_ms = ms_dom / max(n_dom, 1)
 
     S = 32 if args.stage == "coarse" else 48  # the coarse mapper renders without gt depth (Mapper.py:600)
-    per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode)
+    per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode, args.fix_fine)
     from nicecore import render_fn as RF
-    per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode, jac=RF._SAVE_JAC)
+    per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode, jac=RF._SAVE_JAC, fix_fine=args.fix_fine)
     fl = per_ray[dominant] * args.rays if dominant in per_ray else None
     by = per_pt_bytes[dominant] * args.rays * S if dominant in per_pt_bytes else None
     roof = None
@@ -469,7 +479,8 @@ def main():
                 "sampling/compositing f64",
         "data": "synthetic",
         "config": {"workload": f"{args.scene} {args.rays} rays x {S} samples per GPU, stage {args.stage}, "
-                               f"{'mapper/BA grads (rays+grids+decoders)' if args.mode == 'ba' else 'tracker grads (rays)'}",
+                               f"{'mapper/BA grads (rays+grids+decoders)' if args.mode == 'ba' else 'tracker grads (rays)'}"
+                               f"{', fix_fine: color-decoder dW only' if args.fix_fine else ''}",
                    "rays_per_gpu": args.rays, "samples_per_ray": S, "stage": args.stage,
                    "mode": args.mode, "grid_layout": args.layout, "parallelism": f"dp{world}",
                    "grid_grads": "sparse rows" if w["sparse"] is not None else "dense",

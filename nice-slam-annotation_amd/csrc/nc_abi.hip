@@ -297,6 +297,26 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
     m.jobs[j].need_grid = grids[k].grad != nullptr;
     m.jobs[j].need_coord = need_coord;
   }
+  {  // k_mlp_dw: the layout's workgroups go to the decoders that want a weight gradient
+     // only (e.g. the Mapper's fix_fine: the color decoder alone); others get none
+    Job sel[MAX_JOBS];
+    int pos[MAX_JOBS], n = 0;
+    for (int j = 0; j < pl.n_jobs; ++j)
+      if (m.jobs[j].need_dw) {
+        sel[n] = m.jobs[j];
+        pos[n++] = j;
+      }
+    if (n > 0 && n < pl.n_jobs) {
+      int32_t o[MAX_JOBS + 1];
+      split_wgs(w.slab_wgs, (P + 31) / 32, sel, n, o);
+      m.dw_off[0] = 0;
+      for (int j = 0, q = 0; j < MAX_JOBS; ++j) {
+        const bool own = q < n && pos[q] == j;
+        m.dw_off[j + 1] = m.dw_off[j] + (own ? o[q + 1] - o[q] : 0);
+        q += own ? 1 : 0;
+      }
+    }
+  }
   std::memcpy(m.grids, grids, sizeof(m.grids));
   std::memcpy(m.dec, dec, sizeof(m.dec));
   m.share_mid = pl.n_jobs >= 2 && pl.jobs[0].kind == K_FINE && pl.jobs[1].kind == K_MID &&

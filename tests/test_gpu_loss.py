@@ -114,6 +114,37 @@ def test_fused_loss_room0_sizes(n_rays, kind, color_term, dyn):
 
 
 @pytest.mark.gpu
+def test_fix_fine_color_decoder_only():
+    """The Mapper's fix_fine (configs/nice_slam.yaml:62, Mapper.py:416-424): only the color
+    decoder requires grad.  k_mlp_dw then runs all its workgroups on the color decoder
+    (nc_abi.hip fill_mlp); its gradient equals the all-decoders run's (1e-6 of max-abs:
+    the slab partition, so the summation order, differs) and no frozen decoder gets one."""
+    from test_gpu_parity import _room0_case
+    sc, grids, params, ro, rd, dep = _room0_case(1000, "color", seed=5)
+    model = build_model(params, sc.bound, sc.bound * 2, "cuda")
+    g = {k: v.cuda().requires_grad_(True) for k, v in grids.items()}
+    ro = ro.cuda().requires_grad_(True)
+    rd = rd.cuda().requires_grad_(True)
+    gt = dep.cuda()
+    gtc = torch.rand(1000, 3, generator=torch.Generator().manual_seed(4)).cuda()
+    r = make_renderer(sc.bound, H=sc.H, W=sc.W)
+    L = r.render_batch_loss(g, model, rd, ro, "cuda", "color", gt, gtc, loss="mapper", color_term=True)[3]
+    L.backward()
+    full = _grads(model, g, ro, rd)
+    for n in ("coarse", "middle", "fine"):
+        for p in getattr(model, n + "_decoder").parameters():
+            p.requires_grad_(False)
+    _compare_fused_unfused(r, "color", model, g, ro, rd, gt, gtc, "mapper", True, False)
+    L = r.render_batch_loss(g, model, rd, ro, "cuda", "color", gt, gtc, loss="mapper", color_term=True)[3]
+    L.backward()
+    part = _grads(model, g, ro, rd)
+    assert all(not k.startswith("param/") or k.startswith("param/color_decoder.") for k in part), sorted(part)
+    assert any(k.startswith("param/color_decoder.") for k in part)
+    bad = {k: rel_err(part[k].cpu(), full[k].cpu()) for k in part if rel_err(part[k].cpu(), full[k].cpu()) > 1e-6}
+    assert not bad, bad
+
+
+@pytest.mark.gpu
 def test_fused_loss_sharded_depth_max():
     """The data-parallel form: a supplied depth_max (the all-reduced max) with the loss."""
     rec, stage, model, g, ro, rd, r = _setup("color_depth")
