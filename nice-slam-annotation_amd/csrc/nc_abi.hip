@@ -159,7 +159,8 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 
 struct Ws {
   size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
-         coef_d = 0, coef_c = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dtemp = 0, dtemp_bytes = 0,
+         coef_d = 0, coef_c = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
+         dtemp_bytes = 0,
          total = 0;
   bool det = false;
   size_t jac = 0;
@@ -258,6 +259,7 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
       w.dval[b] = take((size_t)ne * 4);
     }
     w.dw = take((size_t)ne * 4);
+    w.dpart = take((size_t)(ne + 31) / 32 * 2 * 32 * 4);
     w.dtemp_bytes = det_sort_temp_bytes(ne, vbits + 2);
     w.dtemp = take(w.dtemp_bytes);
   }
@@ -349,6 +351,7 @@ DetBufs det_bufs(void* ws, const Ws& w) {
     d.val[b] = at<uint32_t>(ws, w.dval[b]);
   }
   d.w = at<float>(ws, w.dw);
+  d.part = at<float>(ws, w.dpart);
   d.temp = at<void>(ws, w.dtemp);
   d.temp_bytes = w.dtemp_bytes;
   d.vbits = w.vbits;

@@ -7,9 +7,9 @@
 //   k_det_keys    entry (job, point, corner) -> key (job << vbits | voxel), weight
 //   radix sort    rocprim's stable LSD radix sort of (key, entry id): the entries of
 //                 one voxel end up adjacent, in ascending (point, corner) order
-//   k_det_reduce  the first entry of each voxel run owns the voxel: it sums
-//                 w * d feature over the run, channel per lane, in that order, and
-//                 adds the sum to the gradient (unique owner: no atomics)
+//   k_det_runs /  each voxel run is summed (w * d feature, channel per lane) in
+//   k_det_join    entry order, 32 entries per half-wave, boundary pieces joined in
+//                 order; one writer per voxel (no atomics)
 // The order is the reference's own: ATen's CPU grid_sampler_3d_backward walks points
 // in order and adds each point's 8 corner contributions (gInp += gOut * w), and a
 // voxel is a corner of a point at most once.
@@ -27,17 +27,21 @@ __device__ __forceinline__ nc_grid grid_of(const MlpCtx& m, int kind) {
   return kind == 0 ? m.grids[0] : kind == 1 ? m.grids[1] : kind == 2 ? m.grids[2] : m.grids[3];
 }
 
+// K: uint32_t keys when job and voxel bits fit (vbits + 2 <= 32: every BASELINE grid,
+// C5's 204M-voxel grids included), else uint64_t; the key buffers are sized for 64 bits
+template <typename K>
 __global__ void __launch_bounds__(256) k_det_keys(const MlpCtx m, DetBufs d) {
+  K* keys = reinterpret_cast<K*>(d.key[0]);
   const int j = blockIdx.y;
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= m.P) return;
   const Job job = job_of(m, j);
-  const uint64_t invalid = (uint64_t(1) << (d.vbits + 2)) - 1;
+  const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   const int64_t e0 = ((int64_t)j * m.P + p) * 8;
   if (!job.need_grid) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      d.key[0][e0 + k] = invalid;
+      keys[e0 + k] = invalid;
       d.val[0][e0 + k] = (uint32_t)(e0 + k);
       d.w[e0 + k] = 0.f;
     }
@@ -54,60 +58,178 @@ __global__ void __launch_bounds__(256) k_det_keys(const MlpCtx m, DetBufs d) {
     const uint64_t x = (uint64_t)(c.x0 + (k & 1)), y = (uint64_t)(c.y0 + ((k >> 1) & 1)),
                    z = (uint64_t)(c.z0 + (k >> 2));
     const bool in = (c.inb >> k) & 1u;
-    d.key[0][e0 + k] = in ? (((uint64_t)j << d.vbits) | ((z * H + y) * W + x)) : invalid;
+    keys[e0 + k] = in ? (K)(((uint64_t)j << d.vbits) | ((z * H + y) * W + x)) : invalid;
     d.val[0][e0 + k] = (uint32_t)(e0 + k);
     d.w[e0 + k] = c.w[k];
   }
 }
 
-// thread = (sorted entry e, channel ch); 8 entries per 256-thread block
-__global__ void __launch_bounds__(256) k_det_reduce(const MlpCtx m, DetBufs d, int64_t n) {
-  const int64_t e = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-  const int ch = threadIdx.x & 31;
-  if (e >= n) return;
-  const uint64_t* key = d.key[1];
-  const uint64_t k0 = key[e];
-  const uint64_t invalid = (uint64_t(1) << (d.vbits + 2)) - 1;
-  if (k0 == invalid || (e > 0 && key[e - 1] == k0)) return;
-  float acc = 0.f;
-  for (int64_t q = e; q < n && key[q] == k0; ++q) {
-    const uint32_t ent = d.val[1][q];
-    acc = acc + m.dfeat[(int64_t)(ent >> 3) * 32 + ch] * d.w[ent];
-  }
+// The sorted entries are cut into sub-chunks of DSUB = 32, one per half-wave (lane =
+// channel).  A voxel's run of entries is summed in entry order, one sub-chunk at a
+// time: k_det_runs sums every run piece of its sub-chunk and writes the runs that lie
+// inside it straight to the gradient; a run that crosses a sub-chunk boundary leaves
+// its pieces in DetBufs::part (slot 0: the sub-chunk's first run, slot 1: its last), and
+// k_det_join, in the sub-chunk where the run starts, adds them up in sub-chunk order.
+// Every run has one writer, a hot voxel's thousands of entries are summed 32 at a time
+// in parallel, and the order is fixed by the sort: bit-identical from run to run.
+constexpr int DSUB = 32;
+
+__device__ __forceinline__ uint32_t shfl_key(uint32_t v, int src) { return __shfl(v, src, 32); }
+__device__ __forceinline__ uint64_t shfl_key(uint64_t v, int src) {
+  const unsigned lo = __shfl((unsigned)(v & 0xffffffffu), src, 32);
+  const unsigned hi = __shfl((unsigned)(v >> 32), src, 32);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// the summed run of voxel key k0 into its gradient row.  Plain stores: every voxel of a
+// grid is the key of at most one run (each grid belongs to one job: a decoder samples
+// its own grid with grad, Plan), the run has one writer, and the row was zeroed
+// before the backward (the gather's grad_zero fill, or k_rows_compact for sparse rows)
+__device__ __forceinline__ void det_add(const MlpCtx& m, const DetBufs& d, uint64_t k0, int ch, float acc) {
   const int j = (int)(k0 >> d.vbits);
   const uint64_t v = k0 & ((uint64_t(1) << d.vbits) - 1);
   const nc_grid G = grid_of(m, job_of(m, j).kind);
-  const uint64_t H = (uint64_t)G.dims[1], W = (uint64_t)G.dims[2];
-  const int64_t x = (int64_t)(v % W), y = (int64_t)((v / W) % H), z = (int64_t)(v / (W * H));
   if (G.grad_rows) {  // sparse gradient rows (claimed by the forward)
     const int r = G.grad_rows[v];
-    if (r >= 0) G.grad[(int64_t)r * 32 + ch] += acc;
+    if (r >= 0) G.grad[(int64_t)r * 32 + ch] = acc;
     return;
   }
-  float* dst = G.grad + z * G.grad_stride[1] + y * G.grad_stride[2] + x * G.grad_stride[3] +
-               (int64_t)ch * G.grad_stride[0];
-  *dst = *dst + acc;
+  const int64_t H = G.dims[1], W = G.dims[2];
+  float* dst;
+  if (G.grad_stride[0] == 1 && G.grad_stride[3] == 32 && G.grad_stride[2] == 32 * W && G.grad_stride[1] == 32 * W * H) {
+    dst = G.grad + 32 * (int64_t)v + ch;  // packed channels-last gradient: row v
+  } else {
+    const int64_t x = (int64_t)(v % W), y = (int64_t)((v / W) % H), z = (int64_t)(v / (W * H));
+    dst = G.grad + z * G.grad_stride[1] + y * G.grad_stride[2] + x * G.grad_stride[3] + (int64_t)ch * G.grad_stride[0];
+  }
+  *dst = acc;
+}
+
+// half-wave = sub-chunk s (entries [32 s, 32 s + 32)), lane = channel.  The run sums are
+// formed in registers, parked in LDS, then written by one loop over the runs.
+template <typename K>
+__global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int64_t n) {
+  __shared__ float racc[8][DSUB][32];
+  __shared__ K rkey[8][DSUB];
+  const int hw = threadIdx.x >> 5, ch = threadIdx.x & 31;
+  const int64_t s = (int64_t)blockIdx.x * 8 + hw;
+  const int64_t e0 = s * DSUB;
+  const int cnt = e0 >= n ? 0 : (int)(n - e0 < DSUB ? n - e0 : DSUB);
+  const K* key = reinterpret_cast<const K*>(d.key[1]);
+  const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
+  // the sub-chunk's entries, one per lane (coalesced), then every entry's weighted
+  // feature-gradient row in flight at once
+  const K myk = ch < cnt ? key[e0 + ch] : invalid;
+  const uint32_t ent = ch < cnt ? d.val[1][e0 + ch] : 0u;
+  const float myw = ch < cnt ? d.w[ent] : 0.f;
+  float v[DSUB];
+#pragma unroll
+  for (int i = 0; i < DSUB; ++i) {
+    const uint32_t en = __shfl(ent, i, 32);
+    v[i] = i < cnt ? m.dfeat[(int64_t)(en >> 3) * 32 + ch] * __shfl(myw, i, 32) : 0.f;
+  }
+  int nr = 0;
+  if (cnt > 0) {
+    K cur = shfl_key(myk, 0);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < DSUB; ++i) {
+      if (i < cnt) {
+        const K k = shfl_key(myk, i);
+        if (k != cur) {
+          racc[hw][nr][ch] = acc;
+          if (ch == 0) rkey[hw][nr] = cur;
+          ++nr;
+          cur = k;
+          acc = 0.f;
+        }
+        acc = acc + v[i];
+      }
+    }
+    racc[hw][nr][ch] = acc;
+    if (ch == 0) rkey[hw][nr] = cur;
+    ++nr;
+  }
+  __syncthreads();
+  if (cnt == 0) return;
+  const K prevk = e0 > 0 ? key[e0 - 1] : invalid;
+  const K nextk = e0 + cnt < n ? key[e0 + cnt] : invalid;
+  float* part = d.part + s * 2 * 32 + ch;
+  for (int r = 0; r < nr; ++r) {
+    const K k = rkey[hw][r];
+    if (k == invalid) continue;
+    const float a = racc[hw][r][ch];
+    const bool first = r == 0;
+    const bool before = first && prevk == k;
+    const bool cont = r == nr - 1 && nextk == k;
+    if (!before && !cont) det_add(m, d, (uint64_t)k, ch, a);  // the whole run is in this sub-chunk
+    else part[first ? 0 : 32] = a;
+  }
+}
+
+// half-wave = sub-chunk s: if a run starts in s and continues past it, sum its pieces
+template <typename K>
+__global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int64_t n) {
+  const int64_t s = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int ch = threadIdx.x & 31;
+  const int64_t e0 = s * DSUB;
+  if (e0 >= n) return;
+  const int64_t e1 = e0 + DSUB < n ? e0 + DSUB : n;
+  const K* key = reinterpret_cast<const K*>(d.key[1]);
+  const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
+  const K last = key[e1 - 1];
+  if (last == invalid || e1 >= n || key[e1] != last) return;  // no run continues past s
+  const bool single = key[e0] == last;
+  if (single && e0 > 0 && key[e0 - 1] == last) return;  // it started before s: not the owner
+  float acc = d.part[(s * 2 + (single ? 0 : 1)) * 32 + ch];
+  for (int64_t t = s + 1;; ++t) {
+    acc = acc + d.part[t * 2 * 32 + ch];
+    const int64_t te = (t + 1) * DSUB;
+    if (te >= n || key[te] != last) break;  // the run ends inside t (or at its end)
+  }
+  det_add(m, d, last, ch, acc);
+}
+
+// rocprim's merge-sort path at every size: its onesweep path (taken above 1M items by
+// default) spins on decoupled look-back flags, and inside a replayed hipGraph it hung
+// or returned garbage order here (NC_DETERMINISTIC at C2, 1.15M entries); the merge
+// path is plain block-sort and merge kernels
+using DetSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                 rocprim::default_config, (size_t(1) << 40)>;
+
+template <typename K>
+static size_t sort_temp_bytes(int64_t n_entries, int end_bit) {
+  size_t bytes = 0;
+  if (rocprim::radix_sort_pairs<DetSortConfig>(nullptr, bytes, (K*)nullptr, (K*)nullptr, (uint32_t*)nullptr,
+                                               (uint32_t*)nullptr, (size_t)n_entries, 0, (unsigned)end_bit) != hipSuccess)
+    return 0;
+  return bytes ? bytes : 1;
 }
 
 size_t det_sort_temp_bytes(int64_t n_entries, int end_bit) {
-  size_t bytes = 0;
-  if (rocprim::radix_sort_pairs(nullptr, bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
-                                (uint32_t*)nullptr, (size_t)n_entries, 0, (unsigned)end_bit) != hipSuccess)
-    return 0;
-  return bytes ? bytes : 1;
+  return end_bit <= 32 ? sort_temp_bytes<uint32_t>(n_entries, end_bit) : sort_temp_bytes<uint64_t>(n_entries, end_bit);
+}
+
+template <typename K>
+static int det_scatter(const MlpCtx& m, const DetBufs& d, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_det_keys<K>, dim3((unsigned)((m.P + 255) / 256), m.n_jobs), dim3(256), 0, s, m, d);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  size_t bytes = d.temp_bytes;
+  if (hipError_t e = rocprim::radix_sort_pairs<DetSortConfig>(
+          d.temp, bytes, reinterpret_cast<K*>(d.key[0]), reinterpret_cast<K*>(d.key[1]), d.val[0], d.val[1],
+          (size_t)n, 0, (unsigned)(d.vbits + 2), s))
+    return (int)e;
+  const int64_t nsub = (n + DSUB - 1) / DSUB;
+  hipLaunchKernelGGL(k_det_runs<K>, dim3((unsigned)((nsub + 7) / 8)), dim3(256), 0, s, m, d, n);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  hipLaunchKernelGGL(k_det_join<K>, dim3((unsigned)((nsub + 7) / 8)), dim3(256), 0, s, m, d, n);
+  return (int)hipGetLastError();
 }
 
 int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s) {
   const int64_t n = (int64_t)m.n_jobs * m.P * 8;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_det_keys, dim3((unsigned)((m.P + 255) / 256), m.n_jobs), dim3(256), 0, s, m, d);
-  if (hipError_t e = hipGetLastError()) return (int)e;
-  size_t bytes = d.temp_bytes;
-  if (hipError_t e = rocprim::radix_sort_pairs(d.temp, bytes, d.key[0], d.key[1], d.val[0], d.val[1], (size_t)n, 0,
-                                               (unsigned)(d.vbits + 2), s))
-    return (int)e;
-  hipLaunchKernelGGL(k_det_reduce, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, m, d, n);
-  return (int)hipGetLastError();
+  return d.vbits + 2 <= 32 ? det_scatter<uint32_t>(m, d, n, s) : det_scatter<uint64_t>(m, d, n, s);
 }
 
 }  // namespace nc

@@ -77,6 +77,8 @@ struct DetBufs {
   uint64_t* key[2];          // [n_jobs * P * 8] sort keys in / out
   uint32_t* val[2];          // entry ids in / out
   float* w;                  // [n_jobs * P * 8] trilinear weight of each entry
+  float* part;               // [ceil(entries / 32)][2][32] partial sums of the runs that cross a
+                             // 32-entry sub-chunk boundary (k_det_runs -> k_det_join)
   void* temp;                // rocprim radix-sort scratch
   size_t temp_bytes;
   int32_t vbits;             // bits of the voxel index; key = job << vbits | voxel

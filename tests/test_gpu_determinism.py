@@ -113,3 +113,40 @@ def test_frustum_masked_nonleaf_grids(deterministic):
             continue
         assert vg.grad is not None, k
         assert rel_err(vg.grad.cpu(), ref[mask].cpu()) <= GRAD_TOL, k
+
+
+@pytest.mark.gpu
+def test_deterministic_graph_replay_bitwise(monkeypatch):
+    """NC_DETERMINISTIC inside a replayed hipGraph at the bench size (1000 rays x 48
+    samples x 3 decoders = 1.15M sorted entries, past rocprim's 1M-item switch to its
+    look-back sort, which hung in graph replays: nc_det.hip keeps the merge path): 40
+    replays, every one bit-identical to the eager deterministic gradients."""
+    from nicecore.graph import GraphedStep
+    monkeypatch.setenv("NC_DETERMINISTIC", "1")
+    sc, grids, params, ro, rd, dep = _room0_case(1000, "color", seed=9)
+    model = build_model(params, sc.bound, sc.bound * 2, "cuda")
+    g_g = {k: v.cuda().contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+           for k, v in grids.items()}
+    ro_g, rd_g, gt = ro.cuda().requires_grad_(True), rd.cuda().requires_grad_(True), dep.cuda()
+    r = make_renderer(sc.bound, H=sc.H, W=sc.W)
+    leaves = list(g_g.values()) + list(model.parameters()) + [ro_g, rd_g]
+
+    def body():
+        for t in leaves:
+            t.grad = None
+        d, u, c = r.render_batch_ray(g_g, model, rd_g, ro_g, "cuda", "color", gt)
+        loss = ((gt.double() - d).abs() * (gt > 0).double()).sum() + 0.2 * c.abs().sum()
+        loss.backward()
+        return loss
+
+    body()
+    ref = [t.grad.detach().clone() if t.grad is not None else None for t in leaves]
+    step = GraphedStep(body)
+    for it in range(40):
+        step()
+        if it % 10 == 9:
+            torch.cuda.synchronize()
+            for t, g0 in zip(leaves, ref):
+                assert (g0 is None) == (t.grad is None)
+                if g0 is not None:
+                    assert torch.equal(t.grad, g0)
