@@ -70,6 +70,11 @@ def parse():
                     help="split the backward (render_fn.DeferParamGrads) so the grid-gradient "
                          "all-reduce overlaps the decoder weight gradients; auto = on for N > 1 "
                          "(BA mode, dense grid gradients)")
+    ap.add_argument("--frustum", default="auto", choices=["auto", "on", "off"],
+                    help="N > 1 grid-gradient exchange over the voxels of the current frame's frustum "
+                         "only (the Mapper's frustum_feature_selection, configs/nice_slam.yaml:74, "
+                         "Mapper.py:371-414: the other voxels are not optimised); auto = on for N > 1 "
+                         "(BA mode, dense channels-last grid gradients)")
     ap.add_argument("--iteration", action="store_true",
                     help="also time the whole Mapper iteration with the Adam step (nicecore.optim.Adam, "
                          "capturable) in the same hipGraph; reported as mapper_iteration_ms")
@@ -101,7 +106,31 @@ def setup_dist(args):
     return world, rank, local
 
 
-def build_workload(args, rank, device):
+def frustum_rows(sc, grids, device):
+    """Voxel rows of each optimised grid inside the current frame's frustum
+    (nicecore.frustum, Mapper.get_mask_from_c2w): the camera is the first synthetic pose
+    of rank 0's seed on every rank, so all ranks exchange the same rows; the depth image
+    is the bound's diagonal everywhere (no surface in front of the walls), so the depth
+    test keeps the whole frustum inside the bound."""
+    from nicecore import scene as S
+    from nicecore.frustum import FrustumSelector
+    poses = []
+    S.synth_rays(sc, 1, seed=1000, poses_out=poses)
+    R, t = poses[0]
+    c2w = torch.eye(4)
+    c2w[:3, :3], c2w[:3, 3] = R, t
+    depth = torch.full((sc.H, sc.W), float((sc.bound[:, 1] - sc.bound[:, 0]).norm()))
+    sel = FrustumSelector(sc.bound, sc.H, sc.W, sc.fx, sc.fy, sc.cx, sc.cy, device)
+    rows = {}
+    for k, g in grids.items():
+        if k == "grid_coarse" or not g.requires_grad:
+            continue
+        m = sel.grid_mask(c2w, k, g.shape[2:], depth)  # [Z, Y, X]
+        rows[k] = m.reshape(-1).nonzero().squeeze(1)
+    return rows
+
+
+def build_workload(args, rank, device, world=1):
     from nicecore import decoder as D
     from nicecore import scene as S
     from nicecore.renderer import Renderer
@@ -138,9 +167,13 @@ def build_workload(args, rank, device):
         from nicecore.sparse import SparseGridGrads
         # rows for every corner of every lookup of one step: no growth after the first step
         sparse = SparseGridGrads(grids, capacity=8 * args.rays * 48)
+    frustum = None
+    if (ba and sparse is None and args.layout == "channels_last" and
+            (args.frustum == "on" or (args.frustum == "auto" and world > 1))):
+        frustum = frustum_rows(sc, grids, device)
     w = dict(sc=sc, grids=grids, model=model, renderer=renderer,
              ro=ro.to(device).requires_grad_(True), rd=rd.to(device).requires_grad_(True),
-             gt=dep.to(device), gtc=col.to(device), ba=ba, sparse=sparse)
+             gt=dep.to(device), gtc=col.to(device), ba=ba, sparse=sparse, frustum=frustum)
     return w
 
 
@@ -193,9 +226,20 @@ def make_step(w, args, world, device):
         loss.backward(one)  # = loss.backward(), without a fill kernel per step
         return loss
 
+    frustum = w["frustum"]
+    gkeys = [k for k, g in grids.items() if g.requires_grad and (sparse is None or k not in sparse.rows)]
+
+    def grid_exchange_async():
+        if frustum is None:  # one RCCL SUM over the core's shared gradient buffer
+            return ND.allreduce_grads_async(gvals)
+        # the frustum's voxel rows only (Mapper frustum feature selection): one RCCL SUM
+        return ND.allreduce_rows_async([(grids[k].grad, frustum[k]) for k in gkeys
+                                        if k in frustum and grids[k].grad is not None])
+
     def post():
-        if world > 1 and w["ba"]:  # one RCCL SUM over the core's shared gradient buffer
-            ND.allreduce_grads(gvals + params)
+        if world > 1 and w["ba"]:
+            grid_exchange_async()()
+            ND.allreduce_grads(params)
             if sparse is not None:  # union of the ranks' touched voxels, then one SUM per grid
                 sparse.allreduce()
 
@@ -205,7 +249,7 @@ def make_step(w, args, world, device):
     def split_post(run_tail):
         # grid gradients are final: start their all-reduce, compute the weight
         # gradients meanwhile, then reduce those (small) once they exist
-        finish = ND.allreduce_grads_async(gvals) if world > 1 else (lambda: None)
+        finish = grid_exchange_async() if world > 1 else (lambda: None)
         run_tail()
         finish()
         if world > 1:
@@ -388,7 +432,7 @@ def main():
     device = torch.device("cuda", torch.cuda.current_device())
     from nicecore import _lib as L
     L.load()
-    w = build_workload(args, rank, device)
+    w = build_workload(args, rank, device, world)
     eager, graphed = make_step(w, args, world, device)
     w["body"] = getattr(make_step, "last_body", None)
     for _ in range(args.warmup):
@@ -484,6 +528,11 @@ def main():
                    "rays_per_gpu": args.rays, "samples_per_ray": S, "stage": args.stage,
                    "mode": args.mode, "grid_layout": args.layout, "parallelism": f"dp{world}",
                    "grid_grads": "sparse rows" if w["sparse"] is not None else "dense",
+                   "grid_exchange": (None if world == 1 else "sparse row union" if w["sparse"] is not None else
+                                     "dense" if w["frustum"] is None else
+                                     "frustum rows (Mapper frustum_feature_selection): %d of %d voxels" % (
+                                         sum(int(v.numel()) for v in w["frustum"].values()),
+                                         sum(int(w["grids"][k][0, 0].numel()) for k in w["frustum"]))),
                    "overlap": "grid all-reduce beside k_mlp_dw" if (w["ba"] and w["sparse"] is None and (
                        args.overlap == "on" or (args.overlap == "auto" and world > 1))) else "none"},
         "roofline": roof,

@@ -124,3 +124,40 @@ def allreduce_grads_async(tensors, group=None, bucket_bytes: int = 4 << 20):
                 g.copy_(flat[o:o + n].view_as(g))
                 o += n
     return finish
+
+
+def allreduce_rows_async(pairs, group=None):
+    """SUM all-reduce of selected voxel rows of channels-last grid gradients, the
+    Mapper's frustum feature selection (src/Mapper.py:371-414, configs/nice_slam.yaml
+    ``frustum_feature_selection: True``): only the voxels inside the current frame's
+    frustum are optimisation variables (``val[mask] = val_grad``), so only their rows are
+    exchanged -- SURVEY.md §8e's compacted all-reduce.  ``pairs``: (grad [1, C, D, H, W]
+    in channels_last_3d, int64 voxel indices in the grid's z-y-x order).  Rows are
+    gathered into one flat buffer (one collective), reduced asynchronously, and written
+    back by the returned ``finish()``; other rows keep the rank-local values."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return lambda: None
+    views = []
+    for g, idx in pairs:
+        v = g.permute(0, 2, 3, 4, 1)
+        if not v.is_contiguous():
+            raise ValueError("allreduce_rows_async needs channels_last_3d gradients")
+        views.append((v.reshape(-1, g.shape[1]), idx))
+    if not views:
+        return lambda: None
+    C = views[0][0].shape[1]
+    n = sum(int(idx.numel()) for _, idx in views)
+    flat = torch.empty(n, C, dtype=views[0][0].dtype, device=views[0][0].device)
+    o = 0
+    for v, idx in views:
+        torch.index_select(v, 0, idx, out=flat[o:o + idx.numel()])
+        o += idx.numel()
+    h = dist.all_reduce(flat, group=group, async_op=True)
+
+    def finish():
+        h.wait()
+        o = 0
+        for v, idx in views:
+            v.index_copy_(0, idx, flat[o:o + idx.numel()])
+            o += idx.numel()
+    return finish

@@ -199,7 +199,7 @@ def ray_exit_t(bound: torch.Tensor, rays_o: torch.Tensor, rays_d: torch.Tensor):
 
 
 def synth_rays(scene: SceneSpec, n_rays: int, n_poses: int = 40, seed: int = 1,
-               edge: int = 0, zero_depth_frac: float = 0.1, outside_frac: float = 0.0):
+               edge: int = 0, zero_depth_frac: float = 0.1, outside_frac: float = 0.0, poses_out=None):
     """Seeded synthetic rays per SURVEY.md §8(d).
 
     Camera centres uniform in the central 60% of the bound, random unit-quaternion
@@ -208,7 +208,8 @@ def synth_rays(scene: SceneSpec, n_rays: int, n_poses: int = 40, seed: int = 1,
     exact zeros; gt_color ~ U(0,1).  ``outside_frac`` of the cameras are placed
     just outside the bound looking in, so some samples fall out of bound.
     Rays that fail the callers' bbox filter (t_exit >= gt_depth) are redrawn.
-    Returns float32 CPU tensors rays_o [N,3], rays_d [N,3], gt_depth [N], gt_color [N,3].
+    Returns float32 CPU tensors rays_o [N,3], rays_d [N,3], gt_depth [N], gt_color [N,3];
+    ``poses_out`` (a list), if given, receives the cameras' (R, t) (c2w = [R | t]).
     """
     gen = torch.Generator().manual_seed(seed)
     b = scene.bound.float()
@@ -233,6 +234,8 @@ def synth_rays(scene: SceneSpec, n_rays: int, n_poses: int = 40, seed: int = 1,
         else:
             t = ctr + (torch.rand(3, generator=gen) - 0.5) * 0.6 * span
         poses.append((R, t))
+    if poses_out is not None:
+        poses_out.extend(poses)
     out_o, out_d, out_dep = [], [], []
     need = n_rays
     while need > 0:

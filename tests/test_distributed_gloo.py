@@ -174,3 +174,51 @@ def test_shared_buffer_ranges():
     assert ranges[0].data_ptr() == buf.data_ptr() and ranges[0].dim() == 1
     ranges, rest = ND._shared_bases([p2, p1, p3, other])
     assert sorted(r.numel() for r in ranges) == [8, 16] and len(rest) == 1
+
+
+def _rows_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import conftest  # noqa: F401  (paths)
+    from nicecore import distributed as ND
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    gen = torch.Generator().manual_seed(rank)
+    grads = [torch.randn(1, 32, 3, 4, 5, generator=gen).contiguous(memory_format=torch.channels_last_3d),
+             torch.randn(1, 32, 2, 3, 2, generator=gen).contiguous(memory_format=torch.channels_last_3d)]
+    before = [g.clone() for g in grads]
+    rows = [torch.tensor([0, 7, 8, 59]), torch.tensor([3, 11])]
+    finish = ND.allreduce_rows_async(list(zip(grads, rows)))
+    finish()
+    out.put((rank, [b.numpy().copy() for b in before], [g.numpy().copy() for g in grads]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_rows_frustum():
+    """Frustum-compacted exchange (bench.py N > 1): the selected voxel rows of every
+    grid are summed over the ranks, the other rows keep each rank's own values."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict((r, (b, a)) for r, b, a in (q.get(timeout=120) for _ in range(world)))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rows = [[0, 7, 8, 59], [3, 11]]
+    for gi in range(2):
+        tot = res[0][0][gi] + res[1][0][gi]
+        for r in range(world):
+            before, after = res[r][0][gi], res[r][1][gi]
+            flat_b = np.moveaxis(before, 1, -1).reshape(-1, 32)
+            flat_a = np.moveaxis(after, 1, -1).reshape(-1, 32)
+            flat_t = np.moveaxis(tot, 1, -1).reshape(-1, 32)
+            sel = np.zeros(flat_b.shape[0], bool)
+            sel[rows[gi]] = True
+            np.testing.assert_allclose(flat_a[sel], flat_t[sel], rtol=0, atol=1e-6)
+            np.testing.assert_array_equal(flat_a[~sel], flat_b[~sel])
