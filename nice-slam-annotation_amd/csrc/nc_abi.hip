@@ -298,6 +298,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
     m.jobs[j].need_dw = dec[k].grad != nullptr;
     m.jobs[j].need_grid = grids[k].grad != nullptr;
     m.jobs[j].need_coord = need_coord;
+    m.jobs[j].keep_h = 1;
   }
   {  // k_mlp_dw: the layout's workgroups go to the decoders that want a weight gradient
      // only (e.g. the Mapper's fix_fine: the color decoder alone); others get none
@@ -405,7 +406,8 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   if (a->stage == NC_STAGE_COARSE && a->gt_depth) return fail(-1, "nicecore: stage 'coarse' ignores gt_depth; pass NULL");
   S = a->n_strat + a->n_surf + a->n_extra;
   P = a->n_rays * S;
-  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC | NC_SAVE_POINT_JACOBIAN | NC_DEFER_PARAM_GRADS))
+  if (a->flags & ~(NC_SAVE_FOR_BACKWARD | NC_DETERMINISTIC | NC_SAVE_POINT_JACOBIAN | NC_DEFER_PARAM_GRADS |
+                   NC_NO_WEIGHT_GRAD_ALL))
     return fail(-1, "nicecore: unknown flags");
   if (a->loss < NC_LOSS_NONE || a->loss > NC_LOSS_TRACKER) return fail(-1, "nicecore: unknown loss " + std::to_string(a->loss));
   if (a->loss != NC_LOSS_NONE) {
@@ -643,6 +645,8 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
+  for (int j = 0; j < m.n_jobs; ++j)  // NC_NO_WEIGHT_GRAD: no activation records for k_mlp_dw
+    m.jobs[j].keep_h = (a->flags & NC_NO_WEIGHT_GRAD(m.jobs[j].kind)) ? 0 : 1;
 #ifdef NC_ABL_NO_ZERO_FILL  // timing-only ablation: the gradient buffer is not zeroed
   if (false) {
 #else
@@ -678,6 +682,9 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   const bool need_coord = a->g_rays_o || a->g_rays_d;
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, need_coord);
+  for (int j = 0; j < m.n_jobs; ++j)
+    if (m.jobs[j].need_dw && (a->flags & NC_NO_WEIGHT_GRAD(m.jobs[j].kind)))
+      return fail(-1, "nicecore: a weight gradient was asked for a decoder flagged NC_NO_WEIGHT_GRAD");
   bool any = need_coord;
   for (int j = 0; j < m.n_jobs; ++j) any |= m.jobs[j].need_dw || m.jobs[j].need_grid;
   if (!any) return 0;
@@ -701,6 +708,9 @@ int nc_render_backward_params(const nc_render_args* a, void* ws, size_t ws_bytes
   fill_ray(rc, a, pl, ws, w, P, S);
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
+  for (int j = 0; j < m.n_jobs; ++j)
+    if (m.jobs[j].need_dw && (a->flags & NC_NO_WEIGHT_GRAD(m.jobs[j].kind)))
+      return fail(-1, "nicecore: a weight gradient was asked for a decoder flagged NC_NO_WEIGHT_GRAD");
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
   bool any_dw = false;
   for (int j = 0; j < m.n_jobs; ++j) any_dw |= m.jobs[j].need_dw != 0;

@@ -16,6 +16,7 @@ struct Job {
   int32_t need_dw;     // decoder parameter gradient
   int32_t need_grid;   // gradient into its own grid (the fine decoder's middle lookup never has one)
   int32_t need_coord;  // gradient into the sample points
+  int32_t keep_h;      // forward: store the activation records h_0..h_4 (k_mlp_dw's operands)
   int32_t c_stride;    // floats between consecutive points' features in MlpCtx::cfeat
   int64_t rec_off;     // float offset of this job's point records in MlpCtx::rec
   int64_t c_off;       // float offset of point 0's features in MlpCtx::cfeat

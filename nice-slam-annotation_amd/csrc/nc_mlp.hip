@@ -379,7 +379,7 @@ __device__ __forceinline__ bool mask_bit(unsigned lo, unsigned hi, int L, int j)
 
 template <int KIND, int T>
 __device__ __forceinline__ void wave_forward(const float* lds, int i, int g, WaveRegs<KIND> (&R)[T],
-                                             float (&out)[T][4], float* const (&rec)[T]) {
+                                             float (&out)[T][4], float* const (&rec)[T], bool keep_h) {
   // R[t].pf / R[t].c: the tiles' inputs (grid features of decoder.py:179-188 /
   // :196-202, interpolated by k_grid_gather), loaded by the caller.  rec[t] != nullptr:
   // the point's activation record (Rec<KIND>) is written as each piece is produced.
@@ -482,7 +482,7 @@ __device__ __forceinline__ void wave_forward(const float* lds, int i, int g, Wav
 #pragma unroll
         for (int j = 0; j < 8; ++j) R[t].h2[j] = R[t].h[j];
       }
-      if (rec[t]) store_rows<2>(rec[t] + Rec<KIND>::H + HID * L, R[t].h, g);
+      if (rec[t] && keep_h) store_rows<2>(rec[t] + Rec<KIND>::H + HID * L, R[t].h, g);
     }
   }
 #pragma unroll
@@ -519,7 +519,7 @@ struct WaveIn {
 
 template <int KIND, int T>
 __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, const WaveIn<KIND> (&R)[T],
-                                               float (&out)[T][4], float* const (&rec)[T]) {
+                                               float (&out)[T][4], float* const (&rec)[T], bool keep_h) {
   using N = Net<KIND>;
   using H = NetH<KIND>;
   constexpr int CB = N::CD / 32;
@@ -608,7 +608,7 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
         h2h[t] = xh[t];
         h2l[t] = xl[t];
       }
-      if (rec[t]) store_rows<2>(rec[t] + Rec<KIND>::H + HID * L, h[t], g);
+      if (rec[t] && keep_h) store_rows<2>(rec[t] + Rec<KIND>::H + HID * L, h[t], g);
     }
   }
 #pragma unroll
@@ -699,9 +699,9 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     load_inputs(blk + nwg);
     float out[T][4];
 #ifdef NC_FWD_F32
-    wave_forward<KIND, T>(lds, i, g, R, out, rec);
+    wave_forward<KIND, T>(lds, i, g, R, out, rec, job.keep_h != 0);
 #else
-    wave_forward_h<KIND, T>(reinterpret_cast<const char*>(lds), i, g, R, out, rec);
+    wave_forward_h<KIND, T>(reinterpret_cast<const char*>(lds), i, g, R, out, rec, job.keep_h != 0);
 #endif
 #pragma unroll
     for (int t = 0; t < T; ++t) {

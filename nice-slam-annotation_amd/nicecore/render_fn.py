@@ -401,6 +401,11 @@ class NiceRenderFn(torch.autograd.Function):
         a = L.NcRenderArgs.from_buffer_copy(
             plan.render_template(device, spec["n_strat"], spec["n_surf"], spec["bound"]))
         a.flags = _flags(ctx, spec, (1, 2))
+        if a.flags & L.NC_SAVE_FOR_BACKWARD:  # decoders without a weight gradient: no activation records
+            sl = plan.param_slices()
+            for k in plan.decs:
+                if not any(ctx.needs_input_grad[8 + sl[k][0]:8 + sl[k][1]]):
+                    a.flags |= L.NC_NO_WEIGHT_GRAD(k)
         a.n_rays = N
         a.rays_o = rays_o.data_ptr()
         a.rays_d = rays_d.data_ptr()
