@@ -190,3 +190,19 @@ def test_fused_loss_upstream_scale():
     G1 = _grads(model, g, ro, rd)
     for k in G1:
         assert rel_err(G2[k].cpu(), 2.0 * G1[k].cpu()) <= 1e-6, k
+
+
+@pytest.mark.gpu
+def test_no_weight_grad_flag_is_enforced(monkeypatch):
+    """NC_NO_WEIGHT_GRAD(kind) (include/nicecore.h) spares the forward's activation records
+    of a decoder; a backward that then asks for that decoder's weight gradient must fail
+    loudly instead of reading records that were never written."""
+    from nicecore import _lib as L
+    from nicecore import render_fn as RF
+    rec, stage, model, g, ro, rd, r = _setup("color_depth")
+    gt, gtc = rec["gt_depth"].cuda(), rec["gt_color"].cuda()
+    orig = RF._flags
+    monkeypatch.setattr(RF, "_flags", lambda ctx, spec, ci=(): orig(ctx, spec, ci) | L.NC_NO_WEIGHT_GRAD(3))
+    L_ = r.render_batch_loss(g, model, rd, ro, "cuda", stage, gt, gtc, loss="mapper", color_term=True)[3]
+    with pytest.raises(L.NiceCoreError, match="NC_NO_WEIGHT_GRAD"):
+        L_.backward()
