@@ -171,6 +171,15 @@ def build_workload(args, rank, device, world=1):
     if (ba and sparse is None and args.layout == "channels_last" and
             (args.frustum == "on" or (args.frustum == "auto" and world > 1))):
         frustum = frustum_rows(sc, grids, device)
+        if world > 1:  # every rank must exchange the same rows (else the collective would hang)
+            import torch.distributed as dist
+            mine = torch.tensor([int(v.numel()) for v in frustum.values()] + [int(v.sum()) for v in frustum.values()],
+                                dtype=torch.int64, device=device)
+            lo, hi = mine.clone(), mine.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            if not torch.equal(lo, hi):
+                raise RuntimeError("frustum rows differ across ranks")
     w = dict(sc=sc, grids=grids, model=model, renderer=renderer,
              ro=ro.to(device).requires_grad_(True), rd=rd.to(device).requires_grad_(True),
              gt=dep.to(device), gtc=col.to(device), ba=ba, sparse=sparse, frustum=frustum)
