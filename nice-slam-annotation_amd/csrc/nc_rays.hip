@@ -318,15 +318,16 @@ __global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
 //     loss = sum_mask tmp [+ w * sum_mask |gt_c - color|]
 // One 1024-thread workgroup.  torch.median's lower median (NaN if any tmp is NaN)
 // is a radix select over the float64 bit patterns (tmp >= 0 orders like its bits as
-// unsigned integers): 8 passes of an 8-bit LDS histogram, recomputing tmp from
-// depth/var each pass.  Sums are per-thread strided partials + a fixed-order tree
-// (deterministic).  The colour sum accumulates in float64 and is rounded once to
+// unsigned integers): 8 passes of an 8-bit LDS histogram over keys formed once into
+// LDS (up to 4,096 rays; beyond, tmp is recomputed from depth/var each pass).  Sums
+// are per-thread strided partials + a fixed-order tree (deterministic).  The colour sum accumulates in float64 and is rounded once to
 // float32 (the reference's float32 sum is pairwise; both are within ~1 ulp of exact).
 // The derivatives are autograd's expressions -- AbsBackward's sgn (sgn(0) = sgn(NaN)
 // = 0), DivBackward's 1/s, SubBackward's negation, masked rows 0 -- and go to
 // coef_d / coef_c, which k_composite_bwd scales by the upstream g_loss.
 // ---------------------------------------------------------------------------
 constexpr int LOSS_THREADS = 1024;
+constexpr int LOSS_KEYS = 4096;  // rays whose median keys are held in LDS (32 KB)
 
 __device__ __forceinline__ double sgn_d(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
 __device__ __forceinline__ float sgn_f(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
@@ -349,10 +350,21 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
   const bool col = (c.loss_flags & NC_LOSS_COLOR) != 0;
   double thr = 0.0;
   if (dyn) {
+    // up to LOSS_KEYS rays (the Tracker's batches) the keys are formed once into LDS
+    // (~0 marks NaN); beyond, every pass recomputes tmp from depth / var
+    __shared__ unsigned long long skey[LOSS_KEYS];
+    const bool cached = c.N <= LOSS_KEYS;
     if (tid == 0) {
       sel_prefix = 0ull;
       sel_k = (long long)((c.N - 1) / 2);
       any_nan = 0;
+    }
+    if (cached) {
+      for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
+        double diff, s;
+        const double t = tracker_tmp(c, r, diff, s);
+        skey[r] = isnan(t) ? ~0ull : (unsigned long long)__double_as_longlong(t);
+      }
     }
     unsigned long long pmask = 0ull;
     for (int shift = 56; shift >= 0; shift -= 8) {
@@ -360,13 +372,22 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
       __syncthreads();
       const unsigned long long prefix = sel_prefix;
       for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
-        double diff, s;
-        const double t = tracker_tmp(c, r, diff, s);
-        if (isnan(t)) {
-          any_nan = 1;
-          continue;
+        unsigned long long key;
+        if (cached) {
+          key = skey[r];
+          if (key == ~0ull) {
+            any_nan = 1;
+            continue;
+          }
+        } else {
+          double diff, s;
+          const double t = tracker_tmp(c, r, diff, s);
+          if (isnan(t)) {
+            any_nan = 1;
+            continue;
+          }
+          key = (unsigned long long)__double_as_longlong(t);
         }
-        const unsigned long long key = (unsigned long long)__double_as_longlong(t);
         if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
       }
       __syncthreads();
