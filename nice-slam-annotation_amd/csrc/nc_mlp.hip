@@ -1175,17 +1175,35 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
     // one k-step = NS independent MFMAs + 2 NS reads at immediate offsets; unrolled by
     // 4 with a scheduling barrier per k-step (fully unrolled, the scheduler hoists
     // every k-step's reads and spills)
+    // A wave whose last tile slot is padding (tau >= NT: 12 of 80 slots for the middle /
+    // colour decoders, 8 of 96 for fine) runs NS - 1 chains: the branch is wave-uniform
+    // and each SIMD then carries fewer MFMAs per sub-chunk.
+    auto ksteps = [&](auto nchains) {
+      constexpr int NC = decltype(nchains)::value;
+#pragma unroll 4
+      for (int q = 0; q < DW_NPTS / 4; ++q) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < NC; ++s) {
+          const float av = buf[yrow[s] + 4 * q * LY::RS];
+          acc[s] = mfma4(av, buf[xrow[s] + 4 * q * LY::RS], acc[s]);
+          bsum[s] += av;
+        }
+      }
+    };
 #ifdef NC_ABL_DW_NO_MFMA  // timing-only ablation: no k-steps
     if (false)
 #endif
-#pragma unroll 4
-    for (int q = 0; q < DW_NPTS / 4; ++q) {
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const float av = buf[yrow[s] + 4 * q * LY::RS];
-        acc[s] = mfma4(av, buf[xrow[s] + 4 * q * LY::RS], acc[s]);
-        bsum[s] += av;
+    {
+#ifdef NC_DW_PAD_CHAINS  // A/B: every wave runs NS chains (padding slots read zeros)
+      if constexpr (false) {
+#else
+      if constexpr (NS > 1) {
+#endif
+        if (wv + DW_WAVES * (NS - 1) < TL::NT) ksteps(std::integral_constant<int, NS>{});
+        else ksteps(std::integral_constant<int, NS - 1>{});
+      } else {
+        ksteps(std::integral_constant<int, NS>{});
       }
     }
   }

@@ -42,6 +42,8 @@ VARIANTS = {
     "fwd_t1_1024": ["-DNC_FWD_THREADS=1024"],
     "fwd_t2_768": ["-DNC_FWD_TILES=2"],
     "fwd_cost_macs": ["-DNC_FWD_COST_MACS"],
+    "dw_pad_chains": ["-DNC_DW_PAD_CHAINS"],
+    "gather8": ["-DNC_GATHER_CH=8"],
 }
 # variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
 
