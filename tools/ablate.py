@@ -44,6 +44,12 @@ VARIANTS = {
     "fwd_cost_macs": ["-DNC_FWD_COST_MACS"],
     "dw_pad_chains": ["-DNC_DW_PAD_CHAINS"],
     "gather8": ["-DNC_GATHER_CH=8"],
+    "dw_serial": ["-DNC_DW_SERIAL"],
+    "dw_core": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_STAGE", "-DNC_ABL_DW_NO_EMB", "-DNC_ABL_DW_NO_MASKPASS",
+                "-DNC_ABL_DW_NO_LOAD"],
+    "dw_none": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_STAGE", "-DNC_ABL_DW_NO_EMB", "-DNC_ABL_DW_NO_MASKPASS",
+                "-DNC_ABL_DW_NO_LOAD", "-DNC_ABL_DW_NO_MFMA"],
+    "dw_serial_nomfma": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_MFMA"],
 }
 # variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
 
