@@ -44,6 +44,8 @@ VARIANTS = {
     "fwd_cost_macs": ["-DNC_FWD_COST_MACS"],
     "dw_pad_chains": ["-DNC_DW_PAD_CHAINS"],
     "gather8": ["-DNC_GATHER_CH=8"],
+    "gather_one": ["-DNC_GATHER_ONE_KERNEL"],
+    "gather_minb8": ["-DNC_GATHER_MINB=8"],
     "dw_serial": ["-DNC_DW_SERIAL"],
     "dw_core": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_STAGE", "-DNC_ABL_DW_NO_EMB", "-DNC_ABL_DW_NO_MASKPASS",
                 "-DNC_ABL_DW_NO_LOAD"],
