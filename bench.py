@@ -83,6 +83,10 @@ def parse():
                          "the color decoder's parameters require grad, the ones the Mapper optimises. "
                          "Default: every decoder parameter requires grad, as in the reference, whose "
                          "autograd computes (and never uses) the middle and fine decoder gradients")
+    ap.add_argument("--render-depth", default="target", choices=["target", "none"],
+                    help="render with the loss target as gt_depth (Mapper / Tracker, S = 48) or "
+                         "without one (S = 32: BASELINE configs[0], the reference's CPU plumbing "
+                         "case C1; the loss still compares with the targets)")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -231,7 +235,8 @@ def make_step(w, args, world, device):
         # Mapper.py:603-612 (BA mode) / Tracker.py:117-131 (tracker mode)
         depth, unc, color, loss = renderer.render_batch_loss(
             grids, model, rd, ro, device, args.stage, gt, gtc, **loss_kw, depth_max=dmax,
-            sparse_grads=sparse, defer_param_grads=defer)
+            sparse_grads=sparse, defer_param_grads=defer,
+            render_gt_depth="target" if args.render_depth == "target" else None)
         loss.backward(one)  # = loss.backward(), without a fill kernel per step
         return loss
 
@@ -342,6 +347,12 @@ def algorithmic_bytes_per_point(stage, mode, jac=False, fix_fine=False):
     return {"k_mlp_fwd": fwd, "k_mlp_dx": dx, "k_mlp_dw": dw, "k_grid_gather": gather}
 
 
+def samples_per_ray(args):
+    """32 stratified + 16 surface samples with a gt depth; the coarse mapper (Mapper.py:600)
+    and --render-depth none render without one: 32."""
+    return 32 if (args.stage == "coarse" or args.render_depth == "none") else 48
+
+
 def cpu_baseline(args, seconds):
     """The CPU oracle (torch-CPU restatement of the reference path) on a bounded sample."""
     from oracle import nice_oracle as O
@@ -363,7 +374,8 @@ def cpu_baseline(args, seconds):
             t.grad = None
         ro_ = ro.clone().requires_grad_(True)
         rd_ = rd.clone().requires_grad_(True)
-        d, u, c = O.render_batch_ray(g, prm, dec_b, sc.bound, rd_, ro_, args.stage, dep)
+        d, u, c = O.render_batch_ray(g, prm, dec_b, sc.bound, rd_, ro_, args.stage,
+                                     dep if args.render_depth == "target" else None)
         if kw["loss"] == "mapper":
             loss = O.mapper_loss(d, c, dep, col, kw["w_color_loss"], kw["color_term"])
         else:
@@ -379,7 +391,7 @@ def cpu_baseline(args, seconds):
         if el >= seconds or n >= 50:
             break
     return {"value": args.rays * n / el, "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{n} iterations x {args.rays} rays x 48 samples, stage {args.stage}, "
+            "sample": f"{n} iterations x {args.rays} rays x {samples_per_ray(args)} samples, stage {args.stage}, "
                       f"{args.mode} grads, torch CPU fp32/fp64 oracle, {threads} threads"}
 
 
@@ -494,7 +506,7 @@ def main():
                       f"eagerly just before the graph-replay timed region")
     avg_ms = ms_dom / max(n_dom, 1)
 
-    S = 32 if args.stage == "coarse" else 48  # the coarse mapper renders without gt depth (Mapper.py:600)
+    S = samples_per_ray(args)
     per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode, args.fix_fine)
     from nicecore import render_fn as RF
     per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode, jac=RF._SAVE_JAC, fix_fine=args.fix_fine)
