@@ -171,6 +171,7 @@ struct Ws {
   int vbits = 0;
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
+  bool fuse = false;  // k_mlp_fwd gathers the grid features itself (no k_grid_gather, no feature buffer)
   int slab_wgs = 1;        // total k_mlp_dw workgroups (= slab rows)
   int32_t dw_off[MAX_JOBS + 1] = {0, 0, 0, 0};
   int64_t slab_stride = 0;
@@ -195,8 +196,28 @@ void split_wgs(int total, int64_t blocks, const Job* jobs, int n_jobs, int32_t* 
   for (int j = n_jobs + 1; j <= MAX_JOBS; ++j) off[j] = off[n_jobs];
 }
 
+// a grid whose corner rows k_mlp_fwd's fused gather reads as float4s (device grid_vec_ok)
+static bool host_vec_ok(const nc_grid& G) {
+  return G.data && G.stride[0] == 1 && (reinterpret_cast<uintptr_t>(G.data) & 15u) == 0 &&
+         G.stride[1] % 4 == 0 && G.stride[2] % 4 == 0 && G.stride[3] % 4 == 0;
+}
+
+// every grid the stage's decoders look up (the fine decoder: also grid_middle) is
+// channels-last: the forward's trilinear lookups can run inside k_mlp_fwd
+static bool stage_fuse(const Plan& pl, const nc_grid* grids) {
+#ifdef NC_NO_FUSE_GATHER
+  return false;
+#else
+  for (int j = 0; j < pl.n_jobs; ++j) {
+    const int k = pl.jobs[j].kind;
+    if (!host_vec_ok(grids[k]) || (k == K_FINE && !host_vec_ok(grids[K_MID]))) return false;
+  }
+  return true;
+#endif
+}
+
 void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1,
-            bool jac = false, bool claims = false) {
+            bool jac = false, bool claims = false, bool fuse = false) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -227,6 +248,8 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
     w.coef_c = take((size_t)N * 12);
   }
   w.save = save;
+  // the fused gather (k_mlp_fwd) cannot claim sparse rows or save the Jacobian
+  w.fuse = fuse && !w.claims && !w.has_jac;
   if (save) {
     int64_t r = 0;
     for (int j = 0; j < pl.n_jobs; ++j) {
@@ -234,7 +257,7 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
       r += P * rec_stride(pl.jobs[j].kind);
     }
     w.rec = take((size_t)r * 4);
-  } else {  // forward only: features go to their own buffer
+  } else if (!w.fuse) {  // forward only: k_grid_gather's features go to their own buffer
     int64_t f = 0;
     for (int j = 0; j < pl.n_jobs; ++j) {
       w.rec_off[j] = f;
@@ -334,7 +357,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.dpts = at<double>(ws, w.dpts);
   m.slab = at<float>(ws, w.slab);
   m.rec = w.save ? at<float>(ws, w.rec) : nullptr;
-  m.cfeat = w.save ? m.rec : at<float>(ws, w.feat);
+  m.cfeat = w.save ? m.rec : (w.fuse ? nullptr : at<float>(ws, w.feat));
   m.claim_rows = w.claims;  // only grids with a row map (nc_grid.grad_rows) claim
   if (w.claims) {
     m.claim_cnt = at<int32_t>(ws, w.claim_cnt);
@@ -381,7 +404,14 @@ bool stage_claims(const Plan& pl, const nc_grid* grids) {
 
 // k_grid_gather with sparse-row claims: zero the shard counters, gather (claims),
 // give the claims their rows (k_rows_compact)
+// The forward's trilinear lookups run inside k_mlp_fwd (MlpCtx::fuse_gather) unless the
+// forward also claims sparse gradient rows, saves the Jacobian, or a grid is not
+// channels-last: then k_grid_gather runs first (and zero-fills the gradient buffer).
 int gather_and_claim(MlpCtx& m, const Ws& w, hipStream_t s) {
+  if (w.fuse) {  // (layout: stage_fuse, no claims, no Jacobian)
+    m.fuse_gather = 1;
+    return 0;
+  }
   if (w.claims)
     if (int e = check_hip(hipMemsetAsync(m.claim_cnt, 0, (size_t)MAX_JOBS * CLAIM_SHARDS * 4, s), "claim counters"))
       return e;
@@ -427,7 +457,7 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
   layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w, vbits,
-         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids));
+         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids), stage_fuse(pl, a->grids));
   if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }
@@ -658,8 +688,10 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     m.zero_n4 = a->grad_zero_floats / 4;
   }
   if (int e = gather_and_claim(m, w, s)) return e;
-  m.zero_fill = nullptr;
-  m.zero_n4 = 0;
+  if (!m.fuse_gather) {  // zeroed by k_grid_gather (else by k_mlp_fwd)
+    m.zero_fill = nullptr;
+    m.zero_n4 = 0;
+  }
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
   if (int e = check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd")) return e;
   if (a->loss != NC_LOSS_NONE)
@@ -732,7 +764,7 @@ static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
   layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w, vbits,
-         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids));
+         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids), stage_fuse(pl, a->grids));
   if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }

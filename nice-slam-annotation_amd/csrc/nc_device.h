@@ -298,6 +298,37 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
   }
 }
 
+// gather8 for channels-last grids with half the registers: two batches of 4 corners
+// (offsets from the corner-0 voxel, not Corners::off), same corner order and
+// association, so the result is bit-identical to gather8 / k_grid_gather
+__device__ __forceinline__ void gather8_b2(const nc_grid& G, const Corners& c, int g, float out[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float v[4][8];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * h + kk;
+      const bool in = (c.inb >> k) & 1u;
+      const int64_t o = (c.z0 + (k >> 2)) * G.stride[1] + (c.y0 + ((k >> 1) & 1)) * G.stride[2] +
+                        (c.x0 + (k & 1)) * G.stride[3];
+      const float* base = G.data + (in ? o : 0);
+      const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
+      const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
+      v[kk][0] = a.x; v[kk][1] = a.y; v[kk][2] = a.z; v[kk][3] = a.w;
+      v[kk][4] = b.x; v[kk][5] = b.y; v[kk][6] = b.z; v[kk][7] = b.w;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * h + kk;
+      const bool in = (c.inb >> k) & 1u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[kk][j] * c.w[k] : 0.f);
+    }
+  }
+}
+
 __device__ __forceinline__ bool grid_vec_ok(const nc_grid& G) {
   return G.stride[0] == 1 && ((reinterpret_cast<uintptr_t>(G.data) & 15u) == 0) &&
          (G.stride[1] % 4 == 0) && (G.stride[2] % 4 == 0) && (G.stride[3] % 4 == 0);

@@ -60,6 +60,8 @@ struct MlpCtx {
   int64_t zero_n4;           // caller's gradient buffer, nc_render_args.grad_zero)
   float* jac;                // NC_SAVE_POINT_JACOBIAN: [n_jobs][P][3][32] d own-grid features /
                              // d (ix, iy, iz) (k_grid_gather -> k_mlp_dx), else NULL
+  int32_t fuse_gather;       // k_mlp_fwd gathers its tiles' grid features itself (trilinear lookups
+                             // of k_grid_gather fused; no claims / Jacobian; zero_fill done by it)
   int32_t claim_rows;        // forward for a backward: k_grid_gather claims sparse gradient rows
                              // (nc_grid.grad_rows) of the grids that have a row map
   int32_t* claim_cnt;        // [MAX_JOBS][CLAIM_SHARDS] claims per shard (zeroed per forward)

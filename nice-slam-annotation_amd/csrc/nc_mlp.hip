@@ -638,7 +638,11 @@ __device__ __forceinline__ Job pick_job(const Job (&jobs)[MAX_JOBS], unsigned y)
   return y == 0 ? jobs[0] : (y == 1 ? jobs[1] : jobs[2]);
 }
 
-template <int KIND>
+// FUSE: the tiles' grid features are gathered here (MLP.sample_grid_feature,
+// decoder.py:179-188, and the fine decoder's grid_middle lookup, :196-202: make_corners +
+// gather8, the same arithmetic as k_grid_gather) instead of read from cfeat, and the
+// backward's gradient buffer is zero-filled at the end of the workgroup's tiles.
+template <int KIND, bool FUSE>
 __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float* lds, int64_t wg, int64_t nwg) {
   constexpr int T = FWD_TILES;
   constexpr int CQ = Net<KIND>::CD / 16;
@@ -656,17 +660,22 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
   // inputs of the wave's next tiles (p.float() and the grid features) are loaded one
   // iteration ahead, so their latency hides behind the current tiles' MLP
   float4 nf[T];
-  float4 nc[T][CQ];
+  float4 nc[T][FUSE ? 1 : CQ];
+  float4 nx[T];  // FUSE: normalize_3d_coordinate of the next tiles' points (this decoder's bound)
   auto load_inputs = [&](int64_t blk) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const int64_t p = point(blk, t);
       const bool ok = blk < nblk && p < ctx.P;
       nf[t] = ok ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
-      const float* cf = ctx.cfeat + job.c_off + (ok ? p : 0) * job.c_stride + 4 * g;
+      if constexpr (FUSE) {
+        nx[t] = ok ? ctx.xyz[(int64_t)job.slot * ctx.P + p] : float4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        const float* cf = ctx.cfeat + job.c_off + (ok ? p : 0) * job.c_stride + 4 * g;
 #pragma unroll
-      for (int q = 0; q < CQ; ++q)
-        nc[t][q] = ok ? *reinterpret_cast<const float4*>(cf + 16 * q) : float4{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < CQ; ++q)
+          nc[t][q] = ok ? *reinterpret_cast<const float4*>(cf + 16 * q) : float4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
   load_inputs(wg);
@@ -685,16 +694,35 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     for (int t = 0; t < T; ++t) {
       pt[t] = point(blk, t);
       R[t].pf[0] = nf[t].x; R[t].pf[1] = nf[t].y; R[t].pf[2] = nf[t].z;
+      if constexpr (FUSE) {
+        const float xyz[3] = {nx[t].x, nx[t].y, nx[t].z};
+        {
+          const nc_grid& G = ctx.grids[KIND];
+          Corners co;
+          make_corners(G, xyz, co);
+          gather8_b2(G, co, g, R[t].c);
+        }
+        if constexpr (KIND == K_FINE) {  // [fine | middle]: the no-grad grid_middle lookup
+          const nc_grid& G = ctx.grids[K_MID];
+          Corners co;
+          make_corners(G, xyz, co);
+          gather8_b2(G, co, g, R[t].c + 8);
+        }
+      } else {
 #pragma unroll
-      for (int q = 0; q < CQ; ++q) {
-        R[t].c[4 * q + 0] = nc[t][q].x; R[t].c[4 * q + 1] = nc[t][q].y;
-        R[t].c[4 * q + 2] = nc[t][q].z; R[t].c[4 * q + 3] = nc[t][q].w;
+        for (int q = 0; q < CQ; ++q) {
+          R[t].c[4 * q + 0] = nc[t][q].x; R[t].c[4 * q + 1] = nc[t][q].y;
+          R[t].c[4 * q + 2] = nc[t][q].z; R[t].c[4 * q + 3] = nc[t][q].w;
+        }
       }
 #ifdef NC_ABL_NO_RECSTORE  // timing-only ablation: the forward writes no activation record
       rec[t] = nullptr;
 #else
       rec[t] = (ctx.save_rec && pt[t] < ctx.P) ? ctx.rec + job.rec_off + pt[t] * Rec<KIND>::STRIDE : nullptr;
 #endif
+      if constexpr (FUSE) {  // the features k_mlp_dw reads from the record (k_grid_gather's store)
+        if (rec[t]) store_rows<CQ>(rec[t] + Rec<KIND>::C, R[t].c, g);
+      }
     }
     load_inputs(blk + nwg);
     float out[T][4];
@@ -717,6 +745,13 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
       }
     }
   }
+  if constexpr (FUSE) {  // the backward's gradient buffer (nc_render_args.grad_zero): stores last
+    if (ctx.zero_fill) {
+      const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+      for (int64_t z = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; z < ctx.zero_n4; z += nthr)
+        ctx.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
 }
 
 // job of workgroup b in a 1-D grid split [off[0], off[1]), [off[1], off[2]), ...
@@ -724,6 +759,7 @@ __device__ __forceinline__ int job_of_wg(const int32_t (&off)[MAX_JOBS + 1], int
   return (b >= off[1] ? 1 : 0) + (b >= off[2] ? 1 : 0);
 }
 
+template <bool FUSE>
 __global__ void __launch_bounds__(FWD_THREADS) k_mlp_fwd(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int b = blockIdx.x;
@@ -732,10 +768,10 @@ __global__ void __launch_bounds__(FWD_THREADS) k_mlp_fwd(const MlpCtx ctx) {
   const int o0 = j == 0 ? ctx.fwd_off[0] : (j == 1 ? ctx.fwd_off[1] : ctx.fwd_off[2]);
   const int o1 = j == 0 ? ctx.fwd_off[1] : (j == 1 ? ctx.fwd_off[2] : ctx.fwd_off[3]);
   switch (job.kind) {
-    case K_COARSE: fwd_job<K_COARSE>(ctx, job, lds, b - o0, o1 - o0); break;
-    case K_MID: fwd_job<K_MID>(ctx, job, lds, b - o0, o1 - o0); break;
-    case K_FINE: fwd_job<K_FINE>(ctx, job, lds, b - o0, o1 - o0); break;
-    default: fwd_job<K_COLOR>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_COARSE: fwd_job<K_COARSE, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_MID: fwd_job<K_MID, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_FINE: fwd_job<K_FINE, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
+    default: fwd_job<K_COLOR, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
   }
 }
 
@@ -1317,8 +1353,13 @@ int mlp_blocks_per_cu(int which) {
     int n = 0;
     hipError_t e = hipSuccess;
     if (which == 0) {
-      set_lds(k_mlp_fwd, mlp_fwd_lds_bytes());
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd, FWD_THREADS, mlp_fwd_lds_bytes());
+      set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes());
+      set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes());
+      int n2 = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<false>, FWD_THREADS, mlp_fwd_lds_bytes());
+      if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n2, k_mlp_fwd<true>, FWD_THREADS, mlp_fwd_lds_bytes());
+      n = n2 < n ? n2 : n;
     } else if (which == 1) {
       set_lds(k_mlp_dx<true>, mlp_dx_lds_bytes());
       set_lds(k_mlp_dx<false>, mlp_dx_lds_bytes());
@@ -1360,8 +1401,13 @@ int fwd_tile_cost(int kind) {
 
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
   static int attr = -1;
-  if (attr != 0 && (attr = set_lds(k_mlp_fwd, mlp_fwd_lds_bytes())) != 0) return attr;
-  hipLaunchKernelGGL(k_mlp_fwd, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
+  if (attr != 0 && (attr = set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes()) |
+                           set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes())) != 0)
+    return attr;
+  if (c.fuse_gather)
+    hipLaunchKernelGGL(k_mlp_fwd<true>, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
+  else
+    hipLaunchKernelGGL(k_mlp_fwd<false>, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ def main():
     args = ap.parse_args()
     import bench
     ns = argparse.Namespace(scene=args.scene, layout="channels_last", rays=16, mode="tracker",
-                            sparse_grads="off")
+                            sparse_grads="off", fix_fine=False, frustum="off")
     w = bench.build_workload(ns, 0, "cuda")
     sc, r = w["sc"], w["renderer"]
     grids = {k: v.detach() for k, v in w["grids"].items()}
