@@ -203,10 +203,10 @@ int64_t max_param_count();
 #define NC_FWD_TILES 1
 #endif
 #ifndef NC_FWD_THREADS
-#define NC_FWD_THREADS 768
+#define NC_FWD_THREADS 512
 #endif
 constexpr int FWD_TILES = NC_FWD_TILES;      // 16-point tiles per wave sharing the weight fragments
-constexpr int FWD_THREADS = NC_FWD_THREADS;  // waves per workgroup x 64
+constexpr int FWD_THREADS = NC_FWD_THREADS;  // waves per workgroup x 64 (8: 200 VGPRs, spill-free with the fused gather)
 #ifndef NC_DX_THREADS
 #define NC_DX_THREADS 768
 #endif
