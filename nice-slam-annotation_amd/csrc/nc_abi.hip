@@ -303,8 +303,9 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.slab_stride = w.slab_stride;
   std::memcpy(m.dw_off, w.dw_off, sizeof(m.dw_off));
   {  // k_mlp_fwd split: one wave of resident workgroups, 16-point tiles per wave
-    const int64_t per = FWD_THREADS / 64 * 16 * FWD_TILES;
-    split_wgs(cu_count() * mlp_blocks_per_cu(0), (P + per - 1) / per, pl.jobs, pl.n_jobs, m.fwd_off, fwd_tile_cost);
+    const int64_t per = fwd_threads(w.fuse) / 64 * 16 * FWD_TILES;
+    split_wgs(cu_count() * mlp_blocks_per_cu(w.fuse ? 3 : 0), (P + per - 1) / per, pl.jobs, pl.n_jobs, m.fwd_off,
+              fwd_tile_cost);
   }
   m.save_rec = w.save;
   for (int j = 0; j < pl.n_jobs; ++j) {

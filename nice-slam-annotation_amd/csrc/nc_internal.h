@@ -188,7 +188,7 @@ int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s);
 int mlp_fwd_lds_bytes();
 int mlp_dw_lds_bytes();
 int mlp_dx_lds_bytes();
-int mlp_blocks_per_cu(int which);  // 0 k_mlp_fwd, 1 k_mlp_dx, 2 k_mlp_dw
+int mlp_blocks_per_cu(int which);  // 0 k_mlp_fwd, 1 k_mlp_dx, 2 k_mlp_dw, 3 k_mlp_fwd (fused gather)
 int rec_stride(int kind);  // floats per point of a decoder's [forward | backward] record
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s);  // grid = c.fwd_off[n_jobs]
 int decoder_macs(int kind);  // multiply-adds per point of one decoder's forward
@@ -203,10 +203,16 @@ int64_t max_param_count();
 #define NC_FWD_TILES 1
 #endif
 #ifndef NC_FWD_THREADS
-#define NC_FWD_THREADS 512
+#define NC_FWD_THREADS 768
+#endif
+#ifndef NC_FWD_THREADS_FUSED
+#define NC_FWD_THREADS_FUSED 512
 #endif
 constexpr int FWD_TILES = NC_FWD_TILES;      // 16-point tiles per wave sharing the weight fragments
-constexpr int FWD_THREADS = NC_FWD_THREADS;  // waves per workgroup x 64 (8: 200 VGPRs, spill-free with the fused gather)
+constexpr int FWD_THREADS = NC_FWD_THREADS;  // k_mlp_fwd<false>: waves per workgroup x 64 (157 VGPRs)
+// k_mlp_fwd<true> (trilinear lookups fused): 8 waves, 200 VGPRs, spill-free (12 waves: 39 spills)
+constexpr int FWD_THREADS_FUSED = NC_FWD_THREADS_FUSED;
+__host__ __device__ constexpr int fwd_threads(bool fuse) { return fuse ? FWD_THREADS_FUSED : FWD_THREADS; }
 #ifndef NC_DX_THREADS
 #define NC_DX_THREADS 768
 #endif

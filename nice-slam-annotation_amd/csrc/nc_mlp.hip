@@ -647,9 +647,9 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
   constexpr int T = FWD_TILES;
   constexpr int CQ = Net<KIND>::CD / 16;
 #ifdef NC_FWD_F32
-  load_weights<KIND, PADW_FWD, FWD_THREADS>(lds, ctx.dec[KIND]);
+  load_weights<KIND, PADW_FWD, fwd_threads(FUSE)>(lds, ctx.dec[KIND]);
 #else
-  load_weights_h<KIND, FWD_THREADS>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
+  load_weights_h<KIND, fwd_threads(FUSE)>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
 #endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
@@ -760,7 +760,7 @@ __device__ __forceinline__ int job_of_wg(const int32_t (&off)[MAX_JOBS + 1], int
 }
 
 template <bool FUSE>
-__global__ void __launch_bounds__(FWD_THREADS) k_mlp_fwd(const MlpCtx ctx) {
+__global__ void __launch_bounds__(fwd_threads(FUSE)) k_mlp_fwd(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int b = blockIdx.x;
   const int j = job_of_wg(ctx.fwd_off, b);
@@ -1343,23 +1343,21 @@ static int set_lds(K kernel, int bytes) {
   return (int)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-// resident workgroups per CU of k_mlp_fwd (0), k_mlp_dx (1), k_mlp_dw (2), from the
+// resident workgroups per CU of k_mlp_fwd (0; fused gather: 3), k_mlp_dx (1), k_mlp_dw (2), from the
 // HIP occupancy calculator (registers, LDS, wave slots); cached per device
 int mlp_blocks_per_cu(int which) {
-  static int cache[64][3] = {};
+  static int cache[64][4] = {};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || which < 0 || which > 2) return 1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || which < 0 || which > 3) return 1;
   if (!cache[dev][which]) {
     int n = 0;
     hipError_t e = hipSuccess;
     if (which == 0) {
       set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes());
-      set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes());
-      int n2 = 0;
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<false>, FWD_THREADS, mlp_fwd_lds_bytes());
-      if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n2, k_mlp_fwd<true>, FWD_THREADS, mlp_fwd_lds_bytes());
-      n = n2 < n ? n2 : n;
+    } else if (which == 3) {
+      set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<true>, FWD_THREADS_FUSED, mlp_fwd_lds_bytes());
     } else if (which == 1) {
       set_lds(k_mlp_dx<true>, mlp_dx_lds_bytes());
       set_lds(k_mlp_dx<false>, mlp_dx_lds_bytes());
@@ -1405,7 +1403,7 @@ int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
                            set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes())) != 0)
     return attr;
   if (c.fuse_gather)
-    hipLaunchKernelGGL(k_mlp_fwd<true>, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
+    hipLaunchKernelGGL(k_mlp_fwd<true>, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS_FUSED), mlp_fwd_lds_bytes(), s, c);
   else
     hipLaunchKernelGGL(k_mlp_fwd<false>, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
   return (int)hipGetLastError();
