@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 7
+#define NC_ABI_VERSION 8
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -433,6 +433,72 @@ int nc_points_forward(const nc_points_args* args, void* workspace, size_t worksp
                       void* stream);
 int nc_points_backward(const nc_points_args* args, void* workspace, size_t workspace_bytes,
                        void* stream);
+
+/* ---- iMAP* (ABI v8) ------------------------------------------
+ * The single-MLP scene model of configs/imap.yaml: get_model(nice=False) builds
+ * MLP(dim=3, c_dim=0, color=True, hidden_size=256, skips=[], n_blocks=4)
+ * (src/conv_onet/config.py:28-32, decoder.py:116-219): emb = sin(p.float() @ B)
+ * (B [3,93]), h_0 = relu(W_0 emb + b_0) (W_0 [256,93]), h_l = relu(W_l h_{l-1} + b_l)
+ * (l = 1..3, [256,256]), raw = W_out h_3 + b_out (W_out [4,256]).  Rendering uses
+ * volume density (occupancy: False): alpha = 1 - exp(-relu(raw[...,3]) * dists),
+ * dists = (z_{i+1} - z_i).float() (1e10 after the last sample) * ||rays_d||
+ * (src/common.py:232-247); points outside the renderer bound get raw[...,3] = 100
+ * (Renderer.py:87).  Replaces Renderer.render_batch_ray (Renderer.py:95-262) with
+ * nice=False and Renderer.eval_points (:36-93, decoders(pi, c_grid=None)). */
+#define NC_IMAP_HIDDEN 256
+typedef struct nc_imap_params {
+  const float* fourier_B; /* [3, 93] embedder._B */
+  const float* lin_w[4];  /* pts_linears[l].weight: [256, 93], [256, 256] x 3 */
+  const float* lin_b[4];  /* [256] */
+  const float* out_w;     /* output_linear.weight [4, 256] */
+  const float* out_b;     /* [4] */
+  float* grad;            /* flat gradient in nn.Module.parameters() order (222,747 floats), or NULL */
+} nc_imap_params;
+
+typedef struct nc_imap_render_args {
+  int32_t abi_version;   /* NC_ABI_VERSION */
+  int32_t flags;         /* NC_SAVE_FOR_BACKWARD */
+  int64_t n_rays;
+  int32_t n_strat;       /* N_samples (configs/imap.yaml:107); N_surface is 0 for iMAP* */
+  int32_t n_extra;       /* importance depths merged into the samples (second pass) */
+  const float* rays_o;   /* [N,3] */
+  const float* rays_d;   /* [N,3] */
+  const float* gt_depth; /* [N] or NULL */
+  const float* depth_max;/* optional device scalar: batch-global max(gt_depth) */
+  double bound[3][2];
+  float t_strat[NC_MAX_SAMPLES];
+  nc_imap_params dec;
+  double* depth;         /* [N] */
+  double* var;           /* [N] */
+  float* color;          /* [N,3] */
+  const double* g_depth; /* backward inputs (NULL = zero) */
+  const double* g_var;
+  const float* g_color;
+  float* g_rays_o;       /* backward outputs (NULL = not wanted) */
+  float* g_rays_d;
+  const double* z_extra; /* [N][n_extra] (ABI v6 semantics) */
+  double* z_out;         /* optional [N][S] */
+  float* weights_out;    /* optional [N][S] */
+} nc_imap_render_args;
+
+typedef struct nc_imap_points_args {
+  int32_t abi_version;
+  int32_t flags;         /* NC_SAVE_FOR_BACKWARD */
+  int64_t n_points;
+  const double* pts;     /* [P,3] float64 */
+  nc_imap_params dec;
+  float* raw;            /* [P,4] decoder output (no bound mask: Renderer.eval_points applies it) */
+  const float* g_raw;    /* [P,4] upstream gradient (backward) */
+  double* g_pts;         /* [P,3] or NULL */
+} nc_imap_points_args;
+
+int64_t nc_imap_param_count(void);
+size_t nc_imap_render_workspace_bytes(const nc_imap_render_args* args);
+int nc_imap_render_forward(const nc_imap_render_args* args, void* workspace, size_t workspace_bytes, void* stream);
+int nc_imap_render_backward(const nc_imap_render_args* args, void* workspace, size_t workspace_bytes, void* stream);
+size_t nc_imap_points_workspace_bytes(const nc_imap_points_args* args);
+int nc_imap_points_forward(const nc_imap_points_args* args, void* workspace, size_t workspace_bytes, void* stream);
+int nc_imap_points_backward(const nc_imap_points_args* args, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,13 +37,14 @@ enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
   KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
-  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_ADAM, KID_COUNT
+  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_ADAM, KID_IMAP_GEMM, KID_IMAP_FOURIER, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
-                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce", "k_sample_pdf", "k_adam"};
+                                       "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce", "k_sample_pdf", "k_adam",
+                                       "k_imap_gemm", "k_imap_fourier"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -636,6 +637,9 @@ size_t nc_struct_size(int which) {
     case 7: return sizeof(nc_pdf_args);
     case 8: return sizeof(nc_adam_args);
     case 9: return sizeof(nc_adam_segment);
+    case 10: return sizeof(nc_imap_render_args);
+    case 11: return sizeof(nc_imap_points_args);
+    case 12: return sizeof(nc_imap_params);
   }
   return 0;
 }
@@ -953,6 +957,339 @@ int nc_sparse_rows_merge(const nc_sparse_rows* in, const nc_sparse_rows* out, co
                      return launch_rows_merge(*in, *out, all_voxel, all_count, world, rank_capacity, temp, temp_bytes, s);
                    }),
                    "sparse rows merge");
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// iMAP* (ABI v8): k_ray_setup -> [k_imap_embed -> 4 x k_imap_gemm (bias+ReLU) ->
+// k_imap_gemm (output) -> k_imap_split] -> k_composite_fwd (volume density);
+// backward: k_composite_bwd -> k_imap_dout -> 4 x k_imap_gemm (ReLU mask) ->
+// k_imap_gemm (d emb) -> k_imap_fourier_bwd -> [dW: 6 split-K k_imap_gemm +
+// bias column sums] -> [k_ray_grads].
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int IH = NC_IMAP_HIDDEN;
+// flat parameter offsets, nn.Module.parameters() order of the iMAP* MLP: embedder._B,
+// pts_linears[0..3].(weight, bias), output_linear.(weight, bias)
+struct ImapOff {
+  int64_t B = 0, w[4], b[4], wo, bo, total;
+  ImapOff() {
+    int64_t o = 3 * EMB;
+    for (int l = 0; l < 4; ++l) {
+      w[l] = o;
+      o += (int64_t)IH * (l == 0 ? EMB : IH);
+      b[l] = o;
+      o += IH;
+    }
+    wo = o;
+    o += 4 * IH;
+    bo = o;
+    total = o + 4;
+  }
+};
+
+struct ImapWs {
+  size_t dmax = 0, z = 0, pts = 0, pf = 0, emb = 0, h = 0, raw = 0, occ = 0, rgb = 0;
+  size_t gocc = 0, grgb = 0, dout = 0, dz = 0, demb = 0, dx = 0, dpts = 0, gnorm = 0, total = 0;
+};
+
+void imap_layout(int64_t N, int64_t P, bool rays, bool bwd, ImapWs& w) {
+  size_t o = 0;
+  auto take = [&](size_t& f, size_t bytes) { f = o; o = align256(o + bytes); };
+  if (rays) {
+    take(w.dmax, 4);
+    take(w.z, (size_t)P * 8);
+  }
+  take(w.pts, rays ? (size_t)P * 24 : 0);
+  take(w.pf, (size_t)P * 16);
+  take(w.emb, (size_t)P * EMBP * 4);
+  take(w.h, (size_t)4 * P * IH * 4);
+  take(w.raw, (size_t)P * 16);
+  if (rays) {
+    take(w.occ, (size_t)P * 4);
+    take(w.rgb, (size_t)P * 12);
+  }
+  if (bwd) {
+    if (rays) {
+      take(w.gocc, (size_t)P * 4);
+      take(w.grgb, (size_t)P * 12);
+      take(w.gnorm, (size_t)N * 4);
+      take(w.dout, (size_t)P * 16);
+    }
+    take(w.dz, (size_t)4 * P * IH * 4);
+    take(w.demb, (size_t)P * EMBP * 4);
+    take(w.dx, (size_t)P * EMBP * 4);
+    take(w.dpts, (size_t)P * 24);
+  }
+  w.total = o;
+}
+
+int check_imap_params(const nc_imap_params& d, bool need_grad) {
+  if (!d.fourier_B || !d.out_w || !d.out_b) return fail(-1, "nicecore: iMAP* parameter pointer is NULL");
+  for (int l = 0; l < 4; ++l)
+    if (!d.lin_w[l] || !d.lin_b[l]) return fail(-1, "nicecore: iMAP* parameter pointer is NULL");
+  (void)need_grad;
+  return 0;
+}
+
+ImapGemm gemm(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int64_t N,
+              int64_t K) {
+  ImapGemm g;
+  std::memset(&g, 0, sizeof(g));
+  g.A = A;
+  g.B = B;
+  g.C = C;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  return g;
+}
+
+int run_gemm(const ImapGemm& g, bool a_km, bool b_kn, hipStream_t s) {
+  return check_hip(timed(KID_IMAP_GEMM, s, [&] { return launch_imap_gemm(g, a_km, b_kn, s); }), "k_imap_gemm");
+}
+
+// forward MLP over P points whose p.float() is in ws.pf: emb, h_0..h_3, raw
+int imap_mlp_forward(const nc_imap_params& d, int64_t P, void* ws, const ImapWs& w, float* raw, hipStream_t s) {
+  const float4* pf = at<float4>(ws, w.pf);
+  float* emb = at<float>(ws, w.emb);
+  float* h = at<float>(ws, w.h);
+  if (int e = check_hip(timed(KID_IMAP_FOURIER, s, [&] { return launch_imap_embed(pf, d.fourier_B, P, emb, s); }),
+                        "k_imap_embed"))
+    return e;
+  for (int l = 0; l < 4; ++l) {
+    const float* x = l == 0 ? emb : h + (int64_t)(l - 1) * P * IH;
+    const int64_t K = l == 0 ? EMB : IH;
+    ImapGemm g = gemm(x, l == 0 ? EMBP : IH, d.lin_w[l], K, h + (int64_t)l * P * IH, IH, P, IH, K);
+    g.bias = d.lin_b[l];
+    g.relu = 1;
+    if (int e = run_gemm(g, false, false, s)) return e;
+  }
+  ImapGemm g = gemm(h + 3 * P * IH, IH, d.out_w, IH, raw, 4, P, 4, IH);
+  g.bias = d.out_b;
+  return run_gemm(g, false, false, s);
+}
+
+// backward from d raw [P][4] (dout): ReLU-masked dX chain, Fourier backward, and the
+// weight gradients (overwritten into d.grad) when d.grad != NULL
+int imap_mlp_backward(const nc_imap_params& d, int64_t P, void* ws, const ImapWs& w, const float* dout, double* dpts,
+                      hipStream_t s) {
+  const float4* pf = at<float4>(ws, w.pf);
+  const float* emb = at<float>(ws, w.emb);
+  const float* h = at<float>(ws, w.h);
+  float* dz = at<float>(ws, w.dz);
+  float* demb = at<float>(ws, w.demb);
+  float* dx = d.grad ? at<float>(ws, w.dx) : nullptr;
+  const int64_t PH = P * IH;
+  {  // dz_3 = (dout W_out) . [h_3 > 0]
+    ImapGemm g = gemm(dout, 4, d.out_w, IH, dz + 3 * PH, IH, P, IH, 4);
+    g.mask = h + 3 * PH;
+    g.ldm = IH;
+    if (int e = run_gemm(g, false, true, s)) return e;
+  }
+  for (int l = 3; l >= 1; --l) {  // dz_{l-1} = (dz_l W_l) . [h_{l-1} > 0]
+    ImapGemm g = gemm(dz + l * PH, IH, d.lin_w[l], IH, dz + (l - 1) * PH, IH, P, IH, IH);
+    g.mask = h + (l - 1) * PH;
+    g.ldm = IH;
+    if (int e = run_gemm(g, false, true, s)) return e;
+  }
+  if (dpts || dx) {
+    ImapGemm g = gemm(dz, IH, d.lin_w[0], EMB, demb, EMBP, P, EMB, IH);  // d emb = dz_0 W_0
+    if (int e = run_gemm(g, false, true, s)) return e;
+    if (int e = check_hip(timed(KID_IMAP_FOURIER, s, [&] {
+                            return launch_imap_fourier_bwd(pf, d.fourier_B, P, demb, dx, dpts, s);
+                          }),
+                          "k_imap_fourier_bwd"))
+      return e;
+  }
+  if (!d.grad) return 0;
+  const ImapOff off;
+  if (int e = check_hip(hipMemsetAsync(d.grad, 0, (size_t)off.total * 4, s), "grad memset")) return e;
+  float* G = d.grad;
+  auto dw = [&](const float* A, int64_t lda, int64_t M, const float* B, int64_t ldb, int64_t N, float* C) {
+    ImapGemm g = gemm(A, lda, B, ldb, C, N, M, N, P);
+    g.atomic = 1;
+    return run_gemm(g, true, true, s);
+  };
+  if (int e = dw(dout, 4, 4, h + 3 * PH, IH, IH, G + off.wo)) return e;                    // dW_out = dout^T h_3
+  for (int l = 3; l >= 1; --l)
+    if (int e = dw(dz + l * PH, IH, IH, h + (l - 1) * PH, IH, IH, G + off.w[l])) return e;  // dW_l = dz_l^T h_{l-1}
+  if (int e = dw(dz, IH, IH, emb, EMBP, EMB, G + off.w[0])) return e;                       // dW_0 = dz_0^T emb
+  if (int e = dw(reinterpret_cast<const float*>(pf), 4, 3, dx, EMBP, EMB, G + off.B)) return e;  // dB = pf^T dx
+  if (int e = check_hip(launch_imap_colsum(dout, P, 4, 4, G + off.bo, s), "k_imap_colsum")) return e;
+  for (int l = 0; l < 4; ++l)
+    if (int e = check_hip(launch_imap_colsum(dz + l * PH, P, IH, IH, G + off.b[l], s), "k_imap_colsum")) return e;
+  return 0;
+}
+
+int imap_render_prepare(const nc_imap_render_args* a, ImapWs& w, int64_t& P, int& S) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (a->n_rays < 0) return fail(-1, "nicecore: n_rays < 0");
+  if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
+  if (a->n_extra < 0 || (a->n_extra > 0 && !a->z_extra && a->n_rays > 0))
+    return fail(-1, "nicecore: n_extra > 0 needs z_extra");
+  if (a->n_strat < 1 || a->n_strat + a->n_extra > NC_MAX_SAMPLES)
+    return fail(-1, "nicecore: need 1 <= N_samples, N_samples + n_extra <= 64");
+  S = a->n_strat + a->n_extra;
+  P = a->n_rays * S;
+  imap_layout(a->n_rays, P, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, w);
+  return 0;
+}
+
+void imap_fill_ray(RayCtx& c, const nc_imap_render_args* a, void* ws, const ImapWs& w, int64_t P, int S) {
+  std::memset(&c, 0, sizeof(c));
+  c.N = a->n_rays;
+  c.P = P;
+  c.S = S;
+  c.n_strat = a->n_strat;
+  c.n_surf = 0;
+  c.n_extra = a->n_extra;
+  c.z_extra = a->z_extra;
+  c.z_out = a->z_out;
+  c.weights_out = a->weights_out;
+  c.stage = NC_STAGE_COLOR;
+  c.occ_a = 0;
+  c.occ_b = -1;
+  c.has_rgb = 1;
+  c.n_jobs = 0;
+  c.rays_o = a->rays_o;
+  c.rays_d = a->rays_d;
+  c.gt_depth = a->gt_depth;
+  c.depth_max = a->depth_max ? a->depth_max : at<float>(ws, w.dmax);
+  std::memcpy(c.bound, a->bound, sizeof(c.bound));
+  std::memcpy(c.t_strat, a->t_strat, sizeof(c.t_strat));
+  c.z = at<double>(ws, w.z);
+  c.pts = at<double>(ws, w.pts);
+  c.pf = at<float4>(ws, w.pf);
+  c.occ = at<float>(ws, w.occ);
+  c.rgb = at<float>(ws, w.rgb);
+  c.depth = a->depth;
+  c.var = a->var;
+  c.color = a->color;
+  c.g_depth = a->g_depth;
+  c.g_var = a->g_var;
+  c.g_color = a->g_color;
+  c.g_rays_o = a->g_rays_o;
+  c.g_rays_d = a->g_rays_d;
+  c.density = 1;
+  if (w.gocc || w.dout) {
+    c.gocc = at<float>(ws, w.gocc);
+    c.grgb = at<float>(ws, w.grgb);
+    c.gnorm = at<float>(ws, w.gnorm);
+    c.dpts = at<double>(ws, w.dpts);
+  }
+}
+
+int imap_points_prepare(const nc_imap_points_args* a, ImapWs& w) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (a->n_points < 0) return fail(-1, "nicecore: n_points < 0");
+  if (a->flags & ~NC_SAVE_FOR_BACKWARD) return fail(-1, "nicecore: unknown flags");
+  imap_layout(0, a->n_points, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, w);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t nc_imap_param_count(void) { return ImapOff().total; }
+
+size_t nc_imap_render_workspace_bytes(const nc_imap_render_args* a) {
+  ImapWs w;
+  int64_t P;
+  int S;
+  if (imap_render_prepare(a, w, P, S)) return 0;
+  return w.total;
+}
+
+int nc_imap_render_forward(const nc_imap_render_args* a, void* ws, size_t ws_bytes, void* stream) {
+  ImapWs w;
+  int64_t P;
+  int S;
+  if (int e = imap_render_prepare(a, w, P, S)) return e;
+  if (int e = check_imap_params(a->dec, false)) return e;
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_rays == 0) return 0;
+  if (!a->rays_o || !a->rays_d || !a->depth || !a->var || !a->color)
+    return fail(-1, "nicecore: NULL ray input or output pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  RayCtx rc;
+  imap_fill_ray(rc, a, ws, w, P, S);
+  if (a->gt_depth && !a->depth_max) {
+    if (a->n_rays <= kDmaxLocalRays) {
+      rc.dmax_local = 1;
+    } else if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) {
+      return e;
+    }
+  }
+  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
+  float* raw = at<float>(ws, w.raw);
+  if (int e = imap_mlp_forward(a->dec, P, ws, w, raw, s)) return e;
+  if (int e = check_hip(launch_imap_split(raw, P, at<float>(ws, w.occ), at<float>(ws, w.rgb), s), "k_imap_split"))
+    return e;
+  return check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd");
+}
+
+int nc_imap_render_backward(const nc_imap_render_args* a, void* ws, size_t ws_bytes, void* stream) {
+  ImapWs w;
+  int64_t P;
+  int S;
+  if (int e = imap_render_prepare(a, w, P, S)) return e;
+  if (int e = check_imap_params(a->dec, true)) return e;
+  if (!(a->flags & NC_SAVE_FOR_BACKWARD)) return fail(-1, "nicecore: backward needs NC_SAVE_FOR_BACKWARD");
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_rays == 0) return 0;
+  const bool need_coord = a->g_rays_o || a->g_rays_d;
+  if (!need_coord && !a->dec.grad) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  RayCtx rc;
+  imap_fill_ray(rc, a, ws, w, P, S);
+  if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
+  float* dout = at<float>(ws, w.dout);
+  if (int e = check_hip(launch_imap_dout(rc.gocc, rc.grgb, P, dout, s), "k_imap_dout")) return e;
+  double* dpts = at<double>(ws, w.dpts);
+  if (int e = imap_mlp_backward(a->dec, P, ws, w, dout, need_coord ? dpts : nullptr, s)) return e;
+  if (!need_coord) return 0;
+  rc.n_jobs = 1;  // the decoder's point gradients (one slot)
+  return check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(rc, s); }), "k_ray_grads");
+}
+
+size_t nc_imap_points_workspace_bytes(const nc_imap_points_args* a) {
+  ImapWs w;
+  if (imap_points_prepare(a, w)) return 0;
+  return w.total;
+}
+
+int nc_imap_points_forward(const nc_imap_points_args* a, void* ws, size_t ws_bytes, void* stream) {
+  ImapWs w;
+  if (int e = imap_points_prepare(a, w)) return e;
+  if (int e = check_imap_params(a->dec, false)) return e;
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_points == 0) return 0;
+  if (!a->pts || !a->raw) return fail(-1, "nicecore: NULL pts or raw");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (int e = check_hip(launch_imap_pf(a->pts, a->n_points, at<float4>(ws, w.pf), s), "k_imap_pf")) return e;
+  return imap_mlp_forward(a->dec, a->n_points, ws, w, a->raw, s);
+}
+
+int nc_imap_points_backward(const nc_imap_points_args* a, void* ws, size_t ws_bytes, void* stream) {
+  ImapWs w;
+  if (int e = imap_points_prepare(a, w)) return e;
+  if (int e = check_imap_params(a->dec, true)) return e;
+  if (!(a->flags & NC_SAVE_FOR_BACKWARD)) return fail(-1, "nicecore: backward needs NC_SAVE_FOR_BACKWARD");
+  if (ws_bytes < w.total || !ws) return fail(-1, "nicecore: workspace too small");
+  if (a->n_points == 0) return 0;
+  if (!a->g_raw) return fail(-1, "nicecore: NULL g_raw");
+  if (!a->g_pts && !a->dec.grad) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return imap_mlp_backward(a->dec, a->n_points, ws, w, a->g_raw, a->g_pts, s);
 }
 
 }  // extern "C"

@@ -1,0 +1,239 @@
+// nc_imap.hip — the iMAP* scene MLP (configs/imap.yaml).
+//
+// get_model(nice=False) (src/conv_onet/config.py:28-32) builds one MLP with
+// c_dim = 0, hidden 256, 4 blocks, no skip, colour output (decoder.py:116-219):
+//   emb = sin(p.float() @ B)                       [P, 93]   (decoder.py:26-30)
+//   h_0 = relu(emb W_0^T + b_0), h_l = relu(h_{l-1} W_l^T + b_l)   [P, 256]
+//   raw = h_3 W_out^T + b_out                      [P, 4]
+// Unlike the 32-wide NICE decoders (whole network in one wavefront's registers,
+// nc_mlp.hip), every layer here is a 256-wide GEMM with 65k MACs per point, so
+// each layer is one launch of an LDS-tiled f32 MFMA GEMM (v_mfma_f32_16x16x4_f32,
+// exact f32 products like the reference's fp32 addmm) with the bias / ReLU /
+// ReLU-mask epilogue fused:
+//   forward   h_l   = relu(h_{l-1} W_l^T + b_l)          (A point-major, B = W [n][k])
+//   backward  dz_l  = (dz_{l+1} W_{l+1}) . [h_l > 0]      (B = W [k][n])
+//   weights   dW_l  = dz_l^T h_{l-1}                      (split over points, float atomics)
+// plus the Fourier embedding (forward / backward) and the bias column sums.
+// Activations stay point-major [P][256] in HBM (1 KB per point per layer); at
+// 512 FLOP per 4-byte activation read per layer the GEMMs are MFMA-bound.
+#include <hip/hip_runtime.h>
+
+#include "nc_device.h"
+#include "nc_internal.h"
+
+namespace nc {
+
+constexpr int GT_M = 64, GT_N = 64, GT_K = 16;  // workgroup tile (4 waves x 32 x 32)
+constexpr int GT_LD = GT_M + 4;                 // LDS row pad
+
+// C[m][n] (+)= sum_k A(m,k) B(k,n)
+//   A_KM: A(m,k) = A[k*lda + m]   else A[m*lda + k]
+//   B_KN: B(k,n) = B[k*ldb + n]   else B[n*ldb + k]
+// epilogue: + bias[n]; relu; * (mask[m*ldm + n] > 0); atomic accumulate (split-K).
+template <bool A_KM, bool B_KN>
+__global__ void __launch_bounds__(256) k_imap_gemm(const ImapGemm g) {
+  __shared__ float As[GT_K][GT_LD];
+  __shared__ float Bs[GT_K][GT_LD];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, i = lane & 15, q = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * GT_M;
+  const int64_t n0 = (int64_t)blockIdx.y * GT_N;
+  const int64_t kb = (int64_t)blockIdx.z * g.k_split;
+  const int64_t ke = kb + g.k_split < g.K ? kb + g.k_split : g.K;
+  const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
+  floatx4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
+  for (int64_t k0 = kb; k0 < ke; k0 += GT_K) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // 1024 elements of each operand tile, 4 per thread
+      int kk, mm;
+      if (A_KM) { mm = t & 63; kk = (t >> 6) + 4 * j; } else { kk = t & 15; mm = (t >> 4) + 16 * j; }
+      const int64_t gk = k0 + kk, gm = m0 + mm;
+      float v = 0.f;
+      if (gk < ke && gm < g.M) v = A_KM ? g.A[gk * g.lda + gm] : g.A[gm * g.lda + gk];
+      As[kk][mm] = v;
+      int kn, nn;
+      if (B_KN) { nn = t & 63; kn = (t >> 6) + 4 * j; } else { kn = t & 15; nn = (t >> 4) + 16 * j; }
+      const int64_t hk = k0 + kn, hn = n0 + nn;
+      float w = 0.f;
+      if (hk < ke && hn < g.N) w = B_KN ? g.B[hk * g.ldb + hn] : g.B[hn * g.ldb + hk];
+      Bs[kn][nn] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GT_K; kk += 4) {
+      const float a0 = As[kk + q][wm + i], a1 = As[kk + q][wm + 16 + i];
+      const float b0 = Bs[kk + q][wn + i], b1 = Bs[kk + q][wn + 16 + i];
+      acc[0][0] = mfma4(a0, b0, acc[0][0]);
+      acc[0][1] = mfma4(a0, b1, acc[0][1]);
+      acc[1][0] = mfma4(a1, b0, acc[1][0]);
+      acc[1][1] = mfma4(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+  // D layout: register r of lane (i, q) = C[row 4q + r][col i] of the 16x16 block
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm) {
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) {
+      const int64_t n = n0 + wn + 16 * bn + i;
+      if (n >= g.N) continue;
+      const float bias = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm + 16 * bm + 4 * q + r;
+        if (m >= g.M) continue;
+        float v = acc[bm][bn][r] + bias;
+        if (g.relu) v = v > 0.f ? v : 0.f;
+        if (g.mask && !(g.mask[m * g.ldm + n] > 0.f)) v = 0.f;
+        if (g.atomic) atomicAdd(g.C + m * g.ldc + n, v);
+        else g.C[m * g.ldc + n] = v;
+      }
+    }
+  }
+}
+
+// emb[p][j] = sin(p.float() @ B)[j] for j < 93, 0 for the pad columns 93..95
+__global__ void k_imap_embed(const float4* pf, const float* B, int64_t P, float* emb) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P * EMBP) return;
+  const int64_t p = e / EMBP;
+  const int j = (int)(e - p * EMBP);
+  float v = 0.f;
+  if (j < EMB) {
+    const float4 f = pf[p];
+    const float x = __builtin_fmaf(f.z, B[2 * EMB + j], __builtin_fmaf(f.y, B[EMB + j], f.x * B[j]));
+    v = fourier_sin(x);
+  }
+  emb[e] = v;
+}
+
+// dx[p][j] = demb[p][j] * cos(x_j) (stored for dB = pf^T dx) and d p.float() = B dx
+// -> dpts (float64, the .float() cast's backward).  Thread = point.
+__global__ void k_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, const float* demb, float* dx,
+                                   double* dpts) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const float4 f = pf[p];
+  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+  for (int j = 0; j < EMB; ++j) {
+    const float x = __builtin_fmaf(f.z, B[2 * EMB + j], __builtin_fmaf(f.y, B[EMB + j], f.x * B[j]));
+    const float v = demb[p * EMBP + j] * fourier_cos(x);
+    if (dx) dx[p * EMBP + j] = v;
+    d0 = d0 + B[j] * v;
+    d1 = d1 + B[EMB + j] * v;
+    d2 = d2 + B[2 * EMB + j] * v;
+  }
+  if (dx) {
+#pragma unroll
+    for (int j = EMB; j < EMBP; ++j) dx[p * EMBP + j] = 0.f;
+  }
+  if (dpts) {
+    dpts[p * 3 + 0] = (double)d0;
+    dpts[p * 3 + 1] = (double)d1;
+    dpts[p * 3 + 2] = (double)d2;
+  }
+}
+
+// out[c] += sum_p X[p*ld + c] (bias gradients); block = 256 columns x one point slice
+__global__ void __launch_bounds__(256) k_imap_colsum(const float* X, int64_t P, int ld, int ncols, int64_t per,
+                                                     float* out) {
+  const int c = threadIdx.x;
+  if (c >= ncols) return;
+  const int64_t pb = (int64_t)blockIdx.x * per;
+  const int64_t pe = pb + per < P ? pb + per : P;
+  float s = 0.f;
+  for (int64_t p = pb; p < pe; ++p) s = s + X[p * ld + c];
+  atomicAdd(out + c, s);
+}
+
+// raw [P][4] -> occupancy slot / rgb (RayCtx inputs of k_composite_*)
+__global__ void k_imap_split(const float* raw, int64_t P, float* occ, float* rgb) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const float4 r = reinterpret_cast<const float4*>(raw)[p];
+  occ[p] = r.w;
+  rgb[p * 3 + 0] = r.x;
+  rgb[p * 3 + 1] = r.y;
+  rgb[p * 3 + 2] = r.z;
+}
+
+// d raw [P][4] from k_composite_bwd's (grgb, gocc)
+__global__ void k_imap_dout(const float* gocc, const float* grgb, int64_t P, float* dout) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  reinterpret_cast<float4*>(dout)[p] = float4{grgb[p * 3 + 0], grgb[p * 3 + 1], grgb[p * 3 + 2], gocc[p]};
+}
+
+// points mode prologue: p.float()
+__global__ void k_imap_pf(const double* pts, int64_t P, float4* pf) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  pf[p] = float4{(float)pts[p * 3 + 0], (float)pts[p * 3 + 1], (float)pts[p * 3 + 2], 0.f};
+}
+
+static inline unsigned blocks_of(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+int launch_imap_gemm(const ImapGemm& g, bool a_km, bool b_kn, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return 0;
+  ImapGemm c = g;
+  int splits = 1;
+  if (c.atomic && c.K > 0) {  // split the reduction over points so the chip fills
+    const int64_t tiles = ((c.M + GT_M - 1) / GT_M) * ((c.N + GT_N - 1) / GT_N);
+    const int64_t want = (2048 + tiles - 1) / tiles;
+    const int64_t maxs = (c.K + 255) / 256;
+    splits = (int)(want < maxs ? want : maxs);
+    if (splits < 1) splits = 1;
+    if (splits > 65535) splits = 65535;
+  }
+  c.k_split = ((c.K + splits - 1) / splits + GT_K - 1) / GT_K * GT_K;
+  if (c.k_split < GT_K) c.k_split = GT_K;
+  splits = (int)((c.K + c.k_split - 1) / c.k_split);
+  if (splits < 1) splits = 1;
+  const dim3 grid(blocks_of(c.M, GT_M), blocks_of(c.N, GT_N), (unsigned)splits);
+  if (!a_km && !b_kn) hipLaunchKernelGGL((k_imap_gemm<false, false>), grid, dim3(256), 0, s, c);
+  else if (!a_km && b_kn) hipLaunchKernelGGL((k_imap_gemm<false, true>), grid, dim3(256), 0, s, c);
+  else if (a_km && b_kn) hipLaunchKernelGGL((k_imap_gemm<true, true>), grid, dim3(256), 0, s, c);
+  else hipLaunchKernelGGL((k_imap_gemm<true, false>), grid, dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+
+int launch_imap_embed(const float4* pf, const float* B, int64_t P, float* emb, hipStream_t s) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_imap_embed, dim3(blocks_of(P * EMBP, 256)), dim3(256), 0, s, pf, B, P, emb);
+  return (int)hipGetLastError();
+}
+
+int launch_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, const float* demb, float* dx, double* dpts,
+                            hipStream_t s) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_imap_fourier_bwd, dim3(blocks_of(P, 256)), dim3(256), 0, s, pf, B, P, demb, dx, dpts);
+  return (int)hipGetLastError();
+}
+
+int launch_imap_colsum(const float* X, int64_t P, int ld, int ncols, float* out, hipStream_t s) {
+  if (P <= 0) return 0;
+  int64_t slices = (P + 255) / 256;
+  if (slices > 1024) slices = 1024;
+  const int64_t per = (P + slices - 1) / slices;
+  hipLaunchKernelGGL(k_imap_colsum, dim3(blocks_of(P, (int)per)), dim3(256), 0, s, X, P, ld, ncols, per, out);
+  return (int)hipGetLastError();
+}
+
+int launch_imap_split(const float* raw, int64_t P, float* occ, float* rgb, hipStream_t s) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_imap_split, dim3(blocks_of(P, 256)), dim3(256), 0, s, raw, P, occ, rgb);
+  return (int)hipGetLastError();
+}
+
+int launch_imap_dout(const float* gocc, const float* grgb, int64_t P, float* dout, hipStream_t s) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_imap_dout, dim3(blocks_of(P, 256)), dim3(256), 0, s, gocc, grgb, P, dout);
+  return (int)hipGetLastError();
+}
+
+int launch_imap_pf(const double* pts, int64_t P, float4* pf, hipStream_t s) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_imap_pf, dim3(blocks_of(P, 256)), dim3(256), 0, s, pts, P, pf);
+  return (int)hipGetLastError();
+}
+
+}  // namespace nc

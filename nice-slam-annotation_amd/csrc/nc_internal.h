@@ -157,7 +157,35 @@ struct RayCtx {
   const double* g_loss;
   double* coef_d;            // [N]    d loss / d depth   (k_loss -> k_composite_bwd)
   float* coef_c;             // [N][3] d loss / d colour
+  // iMAP* volume density (occupancy: False, common.py:232-247): alpha = 1 - exp(-relu(raw)
+  // * dists * ||rays_d||); k_composite_bwd writes d loss / d ||rays_d|| per ray to gnorm,
+  // k_ray_grads adds gnorm * rays_d / ||rays_d|| to g_rays_d
+  int32_t density;
+  float* gnorm;              // [N]
 };
+
+// One layer GEMM of the iMAP* MLP (nc_imap.hip): C[m][n] (+)= sum_k A(m,k) B(k,n)
+struct ImapGemm {
+  const float* A;
+  const float* B;
+  float* C;
+  int64_t M, N, K;
+  int64_t lda, ldb, ldc;
+  const float* bias;   // [N] or NULL
+  const float* mask;   // [M][ldm]: output zeroed where mask <= 0 (ReLU backward), or NULL
+  int64_t ldm;
+  int32_t relu;
+  int32_t atomic;      // accumulate with float atomics (split over K)
+  int64_t k_split;     // set by the launcher
+};
+int launch_imap_gemm(const ImapGemm& g, bool a_kmajor, bool b_kn, hipStream_t s);
+int launch_imap_embed(const float4* pf, const float* B, int64_t P, float* emb, hipStream_t s);
+int launch_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, const float* demb, float* dx, double* dpts,
+                            hipStream_t s);
+int launch_imap_colsum(const float* X, int64_t P, int ld, int ncols, float* out, hipStream_t s);
+int launch_imap_split(const float* raw, int64_t P, float* occ, float* rgb, hipStream_t s);
+int launch_imap_dout(const float* gocc, const float* grgb, int64_t P, float* dout, hipStream_t s);
+int launch_imap_pf(const double* pts, int64_t P, float4* pf, hipStream_t s);
 
 struct ParamReduceCtx {
   int32_t n_jobs;

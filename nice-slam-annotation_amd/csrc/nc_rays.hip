@@ -181,6 +181,7 @@ struct SampleState {
   float a, q, T, w;
   float rgb[3];
   bool inb;
+  float dist, nrm, sig, e;  // density mode (iMAP*)
 };
 
 // shared by forward and backward: alpha, exclusive product T, weights
@@ -195,8 +196,18 @@ __device__ __forceinline__ void sample_state(const RayCtx& c, int64_t r, int lan
   if (!s.inb) occ = 100.f;  // Renderer.py:87
 #pragma unroll
   for (int k = 0; k < 3; ++k) s.rgb[k] = c.has_rgb ? c.rgb[p * 3 + k] : 0.f;
-  const float x = 10.f * occ;
-  s.a = 1.f / (1.f + expf(-x));          // torch.sigmoid
+  if (c.density) {  // iMAP*: raw2alpha(raw, dists) = 1 - exp(-relu(raw) * dists) (common.py:232-247)
+    const double zn = __shfl_down(s.z, 1);
+    s.dist = (lane + 1 < c.S) ? (float)(zn - s.z) : 1e10f;  // dists.float(), 1e10 after the last sample
+    const float* d = c.rays_d + r * 3;
+    s.nrm = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);  // torch.norm(rays_d)
+    s.sig = occ;
+    s.e = expf(-(occ > 0.f ? occ : 0.f) * (s.dist * s.nrm));
+    s.a = 1.f - s.e;
+  } else {
+    const float x = 10.f * occ;
+    s.a = 1.f / (1.f + expf(-x));          // torch.sigmoid
+  }
   s.q = act ? (1.f - s.a) + 1e-10f : 1.f; // (1.-alpha + 1e-10)
   // exclusive prefix product over the wavefront (Hillis-Steele on 64 lanes)
   float incl = s.q;
@@ -294,8 +305,17 @@ __global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
   }
   const float gq = s.T * cB;
   const float ga = gw * s.T - gq;
-  const float gy = (ga * (1.f - s.a)) * s.a;  // sigmoid backward
-  float g_occ = gy * 10.f;
+  float g_occ;
+  if (c.density) {
+    // alpha = 1 - exp(-relu(sig) * dist * nrm): d alpha = e * (relu'(sig) dsig * dist * nrm + relu(sig) * dist * dnrm)
+    const float ge = act ? ga * s.e : 0.f;
+    g_occ = s.sig > 0.f ? ge * (s.dist * s.nrm) : 0.f;
+    const float gn = wsum_f(act ? (ge * (s.sig > 0.f ? s.sig : 0.f)) * s.dist : 0.f);
+    if (lane == 0 && c.gnorm) c.gnorm[r] = gn;
+  } else {
+    const float gy = (ga * (1.f - s.a)) * s.a;  // sigmoid backward
+    g_occ = gy * 10.f;
+  }
   if (!s.inb) g_occ = 0.f;
   if (act) {
     const int64_t p = r * c.S + lane;
@@ -484,7 +504,15 @@ __device__ __forceinline__ void ray_grads_body(const RayCtx& c, int64_t block) {
     const double gd = wsum_d(dp[k] * z);
     if (lane == 0) {
       if (c.g_rays_o) c.g_rays_o[r * 3 + k] = (float)go;
-      if (c.g_rays_d) c.g_rays_d[r * 3 + k] = (float)gd;
+      if (c.g_rays_d) {
+        float v = (float)gd;
+        if (c.density && c.gnorm) {  // + d ||rays_d|| / d rays_d (torch.norm backward, 0 at norm 0)
+          const float* d = c.rays_d + r * 3;
+          const float n = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+          v = v + (n > 0.f ? c.gnorm[r] * (d[k] / n) : 0.f);
+        }
+        c.g_rays_d[r * 3 + k] = v;
+      }
     }
   }
 }

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 7
+NC_ABI_VERSION = 8
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
 NC_DEFER_PARAM_GRADS = 8
@@ -124,6 +124,27 @@ class NcAdamSegment(ctypes.Structure):
                 ("step_dev", c_void_p)]
 
 
+class NcImapParams(ctypes.Structure):
+    _fields_ = [("fourier_B", c_void_p), ("lin_w", c_void_p * 4), ("lin_b", c_void_p * 4),
+                ("out_w", c_void_p), ("out_b", c_void_p), ("grad", c_void_p)]
+
+
+class NcImapRenderArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("flags", c_int32), ("n_rays", c_int64),
+                ("n_strat", c_int32), ("n_extra", c_int32),
+                ("rays_o", c_void_p), ("rays_d", c_void_p), ("gt_depth", c_void_p), ("depth_max", c_void_p),
+                ("bound", (c_double * 2) * 3), ("t_strat", c_float * NC_MAX_SAMPLES), ("dec", NcImapParams),
+                ("depth", c_void_p), ("var", c_void_p), ("color", c_void_p),
+                ("g_depth", c_void_p), ("g_var", c_void_p), ("g_color", c_void_p),
+                ("g_rays_o", c_void_p), ("g_rays_d", c_void_p),
+                ("z_extra", c_void_p), ("z_out", c_void_p), ("weights_out", c_void_p)]
+
+
+class NcImapPointsArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("flags", c_int32), ("n_points", c_int64), ("pts", c_void_p),
+                ("dec", NcImapParams), ("raw", c_void_p), ("g_raw", c_void_p), ("g_pts", c_void_p)]
+
+
 NC_ADAM_DENSE = 0
 NC_ADAM_SPARSE_ROWS = 1
 
@@ -149,6 +170,13 @@ EXPORTS = {
     "nc_adam_step": (c_int, [POINTER(NcAdamArgs), c_void_p]),
     "nc_adam_step_multi": (c_int, [POINTER(NcAdamArgs), POINTER(NcAdamSegment), c_int32, c_void_p]),
     "nc_sparse_rows_clear": (c_int, [POINTER(NcSparseRows), c_void_p]),
+    "nc_imap_param_count": (c_int64, []),
+    "nc_imap_render_workspace_bytes": (c_size_t, [POINTER(NcImapRenderArgs)]),
+    "nc_imap_render_forward": (c_int, [POINTER(NcImapRenderArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_imap_render_backward": (c_int, [POINTER(NcImapRenderArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_imap_points_workspace_bytes": (c_size_t, [POINTER(NcImapPointsArgs)]),
+    "nc_imap_points_forward": (c_int, [POINTER(NcImapPointsArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_imap_points_backward": (c_int, [POINTER(NcImapPointsArgs), c_void_p, c_size_t, c_void_p]),
     "nc_sparse_merge_temp_bytes": (c_size_t, [c_int64, c_int64]),
     "nc_sparse_rows_merge": (c_int, [POINTER(NcSparseRows), POINTER(NcSparseRows), c_void_p, c_void_p,
                                      c_int32, c_int64, c_void_p, c_size_t, c_void_p]),
@@ -194,7 +222,8 @@ KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_f
               "k_grid_bwd": 11, "k_mlp_dw": 12, "k_grid_gather": 13, "k_loss": 14, "k_det_scatter": 15,
               "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18,
               "k_rows_clear": 19, "k_rows_merge": 20, "k_rows_compact": 21,
-              "k_param_ray_reduce": 22, "k_sample_pdf": 23, "k_adam": 24}
+              "k_param_ray_reduce": 22, "k_sample_pdf": 23, "k_adam": 24,
+              "k_imap_gemm": 25, "k_imap_fourier": 26}
 
 
 class KernelTimer:

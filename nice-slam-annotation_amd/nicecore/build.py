@@ -24,7 +24,7 @@ CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(HERE, "libnicecore.so")
 SOURCES = ["nc_abi.hip", "nc_rays.hip", "nc_mlp.hip", "nc_grid.hip", "nc_det.hip", "nc_sample.hip", "nc_frustum.hip", "nc_adam.hip",
-           "nc_sparse.hip", "nc_pdf.hip"]
+           "nc_sparse.hip", "nc_pdf.hip", "nc_imap.hip"]
 ARCH = os.environ.get("NICECORE_ARCH", "gfx950")
 
 

@@ -87,6 +87,16 @@ class MLP(nn.Module):
         self.sample_mode = sample_mode
         self.leaky = leaky
 
+    def forward(self, p, c_grid=None):
+        """MLP.forward (decoder.py:190-219) for the iMAP* scene MLP (c_dim = 0, hidden 256,
+        4 blocks, no skip: get_model(nice=False)) on the HIP kernels (nicecore.imap).  The
+        NICE sub-decoders are evaluated together through NICE.forward."""
+        if self.c_dim != 0:
+            raise NotImplementedError("NICE sub-decoders are evaluated through NICE.forward(p, c_grid, stage)")
+        from .imap import eval_points
+        raw = eval_points(self, p)
+        return raw if self.color else raw[:, 3]
+
 
 class MLP_no_xyz(nn.Module):
     """Coarse decoder: grid feature only, skip concat of the feature after block 2
@@ -143,9 +153,10 @@ class NICE(nn.Module):
 
 
 def get_model(cfg, nice=True):
-    """Factory with the signature of src/conv_onet/config.py:4-33 (NICE only)."""
-    if not nice:
-        raise NotImplementedError("nicecore implements the NICE decoders; iMAP* is out of scope")
+    """Factory with the signature of src/conv_onet/config.py:4-33."""
+    if not nice:  # iMAP*: one scene MLP (config.py:28-32)
+        return MLP(dim=cfg['data']['dim'], c_dim=0, color=True, hidden_size=256, skips=[], n_blocks=4,
+                   pos_embedding_method=cfg['model']['pos_embedding_method'])
     return NICE(dim=cfg['data']['dim'], c_dim=cfg['model']['c_dim'], coarse=cfg['coarse'],
                 coarse_grid_len=cfg['grid_len']['coarse'],
                 middle_grid_len=cfg['grid_len']['middle'],
@@ -162,3 +173,12 @@ def build_default_nice(seed: int | None = 0, coarse: bool = True) -> NICE:
     return NICE(dim=3, c_dim=32, coarse_grid_len=2.0, middle_grid_len=0.32,
                 fine_grid_len=0.16, color_grid_len=0.16, hidden_size=32, coarse=coarse,
                 pos_embedding_method='fourier')
+
+
+def build_imap(seed: int | None = 0) -> MLP:
+    """The iMAP* scene MLP of get_model(cfg, nice=False), seeded like the reference under
+    ``torch.manual_seed(seed)``."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    return MLP(dim=3, c_dim=0, color=True, hidden_size=256, skips=[], n_blocks=4,
+               pos_embedding_method='fourier')

@@ -15,13 +15,16 @@ loss expression (Mapper.py:603-612, Tracker.py:117-131) computed in the same lau
 
 Implemented: the NICE decoders with lindisp = False, perturb = 0, occupancy = True
 (configs/nice_slam.yaml:5,121-126) and any N_importance (hierarchical sampling,
-Renderer.py:239-259); anything else raises instead of silently falling back.
+Renderer.py:239-259); iMAP* (slam.nice = False: one scene MLP, occupancy = False volume
+density, N_surface = 0, configs/imap.yaml) through nicecore.imap, plus its ``regulation``
+(Renderer.py:343-409); anything else raises instead of silently falling back.
 """
 from __future__ import annotations
 
 import torch
 
 from . import _lib as L
+from . import imap as _imap
 from .ops import eval_points as _eval_points
 from .ops import render_rays, render_rays_loss
 
@@ -44,11 +47,14 @@ class Renderer(object):
             slam.H, slam.W, slam.fx, slam.fy, slam.cx, slam.cy)
 
     def _check_supported(self):
-        if not self.nice:
-            raise NotImplementedError("nicecore renders NICE decoders only (iMAP* is out of scope)")
-        if self.lindisp or self.perturb > 0. or not self.occupancy:
+        if self.lindisp or self.perturb > 0.:
+            raise NotImplementedError("nicecore implements lindisp=False, perturb=0 (N_importance >= 0)")
+        if self.nice != self.occupancy:
             raise NotImplementedError(
-                "nicecore implements lindisp=False, perturb=0, occupancy=True (N_importance >= 0)")
+                "nicecore renders NICE decoders with occupancy=True (configs/nice_slam.yaml) and the "
+                "iMAP* MLP with volume density, occupancy=False (configs/imap.yaml)")
+        if not self.nice and self.N_surface != 0:
+            raise NotImplementedError("iMAP* renders with N_surface = 0 (configs/imap.yaml:108)")
 
     def eval_points(self, p, decoders, c=None, stage='color', device='cuda:0'):
         """Renderer.py:36-93: NICE.forward plus the strict in-bound mask; points outside
@@ -61,7 +67,7 @@ class Renderer(object):
         out = None
         s = 0
         for pi in torch.split(p, self.points_batch_size):
-            r = _eval_points(decoders, pi, c, stage)
+            r = _eval_points(decoders, pi, c, stage) if self.nice else _imap.eval_points(decoders, pi)
             if out is None:
                 out = torch.empty(p.shape[0], 4, dtype=r.dtype, device=r.device)
             out[s:s + pi.shape[0]] = r
@@ -82,6 +88,9 @@ class Renderer(object):
         self._check_supported()
         if gt_depth is not None:
             gt_depth = gt_depth.reshape(-1)
+        if not self.nice:  # iMAP*: the scene MLP + volume density (nicecore.imap)
+            return _imap.render_rays(decoders, rays_o, rays_d, self.bound, gt_depth, self.N_samples,
+                                     self.N_importance, depth_max)
         return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
                            self.N_samples, self.N_surface, depth_max, sparse_grads=sparse_grads,
                            n_importance=self.N_importance, perturb=self.perturb)
@@ -96,11 +105,29 @@ class Renderer(object):
         render_gt_depth=None if coarse_mapper else 'target'``; Tracker.optimize_cam_in_batch:
         ``loss='tracker', color_term=use_color_in_tracking, handle_dynamic=handle_dynamic``."""
         self._check_supported()
+        if not self.nice:
+            raise NotImplementedError("render_batch_loss fuses the NICE losses; iMAP* callers use render_batch_ray")
         return render_rays_loss(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth.reshape(-1),
                                 loss, gt_color, w_color_loss, color_term, handle_dynamic,
                                 render_gt_depth, self.N_samples, self.N_surface, depth_max,
                                 sparse_grads=sparse_grads, n_importance=self.N_importance,
                                 perturb=self.perturb, defer_param_grads=defer_param_grads)
+
+    def regulation(self, c, decoders, rays_d, rays_o, gt_depth, device, stage='color', t_rand=None):
+        """Renderer.py:343-409 (iMAP* only): densities of N_samples points per ray in
+        [0, 0.85 gt_depth], stratified with random offsets (perturb = 1); the decoder runs on
+        the HIP core (eval_points).  ``t_rand`` ([N, N_samples], default torch.rand) makes the
+        draw reproducible."""
+        S = self.N_samples
+        # near = 0: z = 0 * (1 - t) + far * t == far * t exactly
+        z = (gt_depth.reshape(-1, 1) * 0.85) * torch.linspace(0., 1., steps=S).to(device)
+        mid = .5 * (z[:, 1:] + z[:, :-1])
+        lo, hi = torch.cat([z[:, :1], mid], 1), torch.cat([mid, z[:, -1:]], 1)
+        if t_rand is None:
+            t_rand = torch.rand(z.shape).to(device)
+        z = lo + (hi - lo) * t_rand
+        pts = (rays_o[:, None, :] + rays_d[:, None, :] * z[:, :, None]).reshape(-1, 3)
+        return self.eval_points(pts, decoders, c, stage, device)[:, 3]
 
     def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
         """Renderer.py:264-340: chunked full-image render, no grad."""

@@ -43,6 +43,9 @@ def test_struct_layouts_match(lib):
     assert lib.nc_struct_size(5) == ctypes.sizeof(L.NcFrustumArgs)
     assert lib.nc_struct_size(6) == ctypes.sizeof(L.NcSparseRows)
     assert lib.nc_struct_size(7) == ctypes.sizeof(L.NcPdfArgs)
+    assert lib.nc_struct_size(10) == ctypes.sizeof(L.NcImapRenderArgs)
+    assert lib.nc_struct_size(11) == ctypes.sizeof(L.NcImapPointsArgs)
+    assert lib.nc_struct_size(12) == ctypes.sizeof(L.NcImapParams)
     assert lib.nc_abi_version() == L.NC_ABI_VERSION
 
 
@@ -156,3 +159,9 @@ def test_adam_optimizer_contract():
         Adam(p, amsgrad=True)
     assert _dense_layout(torch.zeros(1, 32, 3, 4, 5).contiguous(memory_format=torch.channels_last_3d))
     assert not _dense_layout(torch.zeros(4, 6)[:, :3])
+
+
+def test_imap_param_count_matches_module(lib):
+    """nc_imap_param_count == the iMAP* MLP's parameter count (config.py:28-32)."""
+    m = D.build_imap(seed=0)
+    assert lib.nc_imap_param_count() == sum(p.numel() for p in m.parameters()) == 222747

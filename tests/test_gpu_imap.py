@@ -1,0 +1,186 @@
+"""iMAP* render path on the HIP core (nicecore.imap, ABI v8) against the reference's
+golden vectors (tests/golden/make_golden_imap.py) and the CPU oracle
+(oracle/imap_oracle.py).  Every call goes through libnicecore.so.
+
+Tolerances (max|got-ref| / max|ref| per tensor): outputs <= 2e-5, gradients <= 2e-4
+(f32 MFMA GEMMs vs MKL addmm summation order; sample points are bit-exact f64).
+"""
+import json
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import imap_oracle as IO
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+META = json.load(open(os.path.join(GOLD, "imap_meta.json")))
+CASES = [c["name"] for c in META["cases"]]
+OUT_TOL, GRAD_TOL = 2e-5, 2e-4
+
+
+def _load(name):
+    with np.load(os.path.join(GOLD, f"imap_{name}.npz")) as z:
+        return {k: torch.from_numpy(z[k]) for k in z.files}
+
+
+def _scene():
+    d = _load("scene")
+    return d["bound"], {k[len("param/"):]: v for k, v in d.items() if k.startswith("param/")}
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _model(params):
+    from nicecore import decoder as D
+    m = D.build_imap(seed=None)
+    m.load_state_dict(params)
+    return m.cuda()
+
+
+def _renderer(bound, n_importance):
+    from nicecore.renderer import Renderer
+    cfg = {"rendering": {"lindisp": False, "perturb": 0.0, "N_samples": META["n_samples"], "N_surface": 0,
+                         "N_importance": n_importance}, "scale": 1, "occupancy": False}
+    slam = types.SimpleNamespace(nice=False, bound=bound, H=64, W=80, fx=60., fy=60., cx=40., cy=32.)
+    return Renderer(cfg, None, slam)
+
+
+def _render(rec, params, bound, n_importance, with_depth, want_params=True):
+    m = _model(params)
+    for p in m.parameters():
+        p.requires_grad_(want_params)
+    r = _renderer(bound, n_importance)
+    ro = rec["rays_o"].cuda().requires_grad_(True)
+    rd = rec["rays_d"].cuda().requires_grad_(True)
+    gt = rec["gt_depth"].cuda() if with_depth else None
+    d, v, c = r.render_batch_ray(None, m, rd, ro, "cuda", "color", gt)
+    torch.autograd.backward([d, v, c], [rec["g_depth"].cuda(), rec["g_var"].cuda(), rec["g_color"].cuda()])
+    torch.cuda.synchronize()
+    return m, (d, v, c), ro, rd
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_imap_render_matches_reference(case):
+    c = next(x for x in META["cases"] if x["name"] == case)
+    bound, params = _scene()
+    rec = _load(case)
+    m, (d, v, col), ro, rd = _render(rec, params, bound, c["n_importance"], c["with_depth"])
+    errs = {"depth": rel(d, rec["depth"]), "var": rel(v, rec["var"]), "color": rel(col, rec["color"])}
+    bad = {k: e for k, e in errs.items() if not e <= OUT_TOL}
+    gerrs = {"rays_o": rel(ro.grad, rec["grad/rays_o"]), "rays_d": rel(rd.grad, rec["grad/rays_d"])}
+    for n, p in m.named_parameters():
+        gerrs[n] = rel(p.grad, rec["grad/param/" + n])
+    bad.update({k: e for k, e in gerrs.items() if not e <= GRAD_TOL})
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_imap_eval_points_matches_reference(case):
+    bound, params = _scene()
+    rec = _load(case)
+    m = _model(params)
+    r = _renderer(bound, 0)
+    with torch.no_grad():
+        raw = r.eval_points(rec["pts"].cuda(), m, None, "color", "cuda")
+    assert raw.dtype == torch.float32 and raw.shape == rec["raw"].shape
+    assert rel(raw, rec["raw"]) <= OUT_TOL
+
+
+@pytest.mark.gpu
+def test_imap_tracker_mode_rays_only():
+    """Tracker: parameters frozen, gradients to the rays only (incl. the ||rays_d|| term of dists)."""
+    c = META["cases"][0]
+    bound, params = _scene()
+    rec = _load(c["name"])
+    m, _, ro, rd = _render(rec, params, bound, c["n_importance"], c["with_depth"], want_params=False)
+    assert rel(ro.grad, rec["grad/rays_o"]) <= GRAD_TOL
+    assert rel(rd.grad, rec["grad/rays_d"]) <= GRAD_TOL
+    assert all(p.grad is None for p in m.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 77, 20000])
+def test_imap_points_forward_backward_vs_oracle(P):
+    """MLP.forward(p) on caller points (ragged sizes, tile tails) and its backward vs autograd
+    through the oracle."""
+    bound, params = _scene()
+    g = torch.Generator().manual_seed(P)
+    p = (torch.rand(P, 3, generator=g, dtype=torch.float64) * 1.2 - 0.1)
+    m = _model(params)
+    pg = p.cuda().requires_grad_(True)
+    raw = m(pg)
+    up = torch.randn(P, 4, generator=g)
+    raw.backward(up.cuda())
+    prm = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    pc = p.clone().requires_grad_(True)
+    ref = IO.imap_forward(pc, prm)
+    ref.backward(up)
+    assert rel(raw, ref) <= OUT_TOL
+    assert rel(pg.grad, pc.grad) <= GRAD_TOL
+    for n, q in m.named_parameters():
+        assert rel(q.grad, prm[n].grad) <= GRAD_TOL, n
+
+
+@pytest.mark.gpu
+def test_imap_bench_size_vs_oracle():
+    """1,000 rays x (32 + 12 importance) samples on the room0 bound: HIP vs the CPU oracle."""
+    from nicecore import scene as S
+    sc = S.make_scene("replica_room0")
+    bound, params = sc.bound, _scene()[1]
+    ro, rd, dep, _ = S.synth_rays(sc, 1000, seed=7)
+    m = _model(params)
+    r = _renderer(bound, 12)
+    rog, rdg = ro.cuda().requires_grad_(True), rd.cuda().requires_grad_(True)
+    d, v, c = r.render_batch_ray(None, m, rdg, rog, "cuda", "color", dep.cuda())
+    (d.sum() + c.sum()).backward()
+    prm = {k: x.clone().requires_grad_(True) for k, x in params.items()}
+    roc, rdc = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
+    dc, vc, cc = IO.render_batch_ray(prm, bound, rdc, roc, dep, 32, 12)
+    (dc.sum() + cc.sum()).backward()
+    assert rel(d, dc) <= 1e-4 and rel(c, cc) <= 1e-4
+    assert rel(rog.grad, roc.grad) <= 1e-3
+    for n, q in m.named_parameters():
+        assert rel(q.grad, prm[n].grad) <= 1e-3, n
+
+
+@pytest.mark.gpu
+def test_imap_regulation_matches_oracle():
+    """Renderer.regulation (Renderer.py:343-409) with a fixed t_rand: densities of the
+    oracle at the same points."""
+    bound, params = _scene()
+    rec = _load(CASES[0])
+    m = _model(params)
+    r = _renderer(bound, 0)
+    N, S = rec["rays_o"].shape[0], META["n_samples"]
+    t_rand = torch.rand(N, S, generator=torch.Generator().manual_seed(3))
+    gt = rec["gt_depth"]
+    sig = r.regulation(None, m, rec["rays_d"].cuda(), rec["rays_o"].cuda(), gt.cuda(), "cuda", t_rand=t_rand.cuda())
+    far = gt.reshape(-1, 1).repeat(1, S) * 0.85
+    z = 0.0 * (1. - torch.linspace(0., 1., S)) + far * torch.linspace(0., 1., S)
+    mids = .5 * (z[..., 1:] + z[..., :-1])
+    z = torch.cat([z[..., :1], mids], -1) + (torch.cat([mids, z[..., -1:]], -1) - torch.cat([z[..., :1], mids], -1)) * t_rand
+    pts = (rec["rays_o"][:, None, :] + rec["rays_d"][:, None, :] * z[..., None]).reshape(-1, 3)
+    with torch.no_grad():
+        ref = IO.eval_points(pts, params, bound)[:, -1]
+    assert rel(sig, ref) <= OUT_TOL
+
+
+@pytest.mark.gpu
+def test_imap_empty_batch():
+    bound, params = _scene()
+    m = _model(params)
+    r = _renderer(bound, 12)
+    ro = torch.zeros(0, 3, device="cuda", requires_grad=True)
+    rd = torch.zeros(0, 3, device="cuda", requires_grad=True)
+    d, v, c = r.render_batch_ray(None, m, rd, ro, "cuda", "color", torch.zeros(0, device="cuda"))
+    (d.sum() + c.sum()).backward()
+    assert d.shape == (0,) and c.shape == (0, 3)
+    assert all(float(p.grad.abs().max()) == 0.0 for p in m.parameters())

@@ -59,3 +59,55 @@ def test_oracle_sample_points_and_raw(case):
         raw = O.eval_points(rec["pts"], {k: v.detach() for k, v in g.items()},
                             {k: v.detach() for k, v in prm.items()}, bound, dec_bounds, stage)
     torch.testing.assert_close(raw, rec["raw"], rtol=0, atol=0)
+
+
+# ---- iMAP* (tests/golden/make_golden_imap.py) ----
+import json  # noqa: E402
+import os  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+from oracle import imap_oracle as IO  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+IMAP_META = json.load(open(os.path.join(GOLD, "imap_meta.json")))
+IMAP_CASES = [c["name"] for c in IMAP_META["cases"]]
+
+
+def load_imap(name):
+    with np.load(os.path.join(GOLD, f"imap_{name}.npz")) as z:
+        return {k: torch.from_numpy(z[k]) for k in z.files}
+
+
+def imap_scene():
+    with np.load(os.path.join(GOLD, "imap_scene.npz")) as z:
+        d = {k: torch.from_numpy(z[k]) for k in z.files}
+    return d["bound"], {k[len("param/"):]: v for k, v in d.items() if k.startswith("param/")}
+
+
+def run_imap_oracle(name):
+    case = next(c for c in IMAP_META["cases"] if c["name"] == name)
+    bound, params = imap_scene()
+    rec = load_imap(name)
+    ro = rec["rays_o"].clone().requires_grad_(True)
+    rd = rec["rays_d"].clone().requires_grad_(True)
+    prm = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    gt = rec["gt_depth"] if case["with_depth"] else None
+    out = IO.render_batch_ray(prm, bound, rd, ro, gt, IMAP_META["n_samples"], case["n_importance"])
+    torch.autograd.backward(list(out), [rec["g_depth"], rec["g_var"], rec["g_color"]])
+    return rec, out, ro, rd, prm, bound
+
+
+@pytest.mark.parametrize("case", IMAP_CASES)
+def test_imap_oracle_outputs_and_grads(case):
+    rec, (depth, var, color), ro, rd, prm, bound = run_imap_oracle(case)
+    torch.testing.assert_close(depth.detach(), rec["depth"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(var.detach(), rec["var"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(color.detach(), rec["color"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(ro.grad, rec["grad/rays_o"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rd.grad, rec["grad/rays_d"], rtol=1e-5, atol=1e-6)
+    for k, v in prm.items():
+        torch.testing.assert_close(v.grad, rec["grad/param/" + k], rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        raw = IO.eval_points(rec["pts"], {k: v.detach() for k, v in prm.items()}, bound)
+    torch.testing.assert_close(raw, rec["raw"], rtol=0, atol=0)
