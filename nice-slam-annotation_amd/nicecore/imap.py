@@ -73,7 +73,7 @@ class ImapRenderFn(torch.autograd.Function):
         a = L.NcImapRenderArgs()
         a.abi_version = L.NC_ABI_VERSION
         need = ctx.needs_input_grad
-        a.flags = L.NC_SAVE_FOR_BACKWARD if (torch.is_grad_enabled() and any(need[1:3] + need[4:])) else 0
+        a.flags = L.NC_SAVE_FOR_BACKWARD if any(need[1:3] + need[4:]) else 0
         a.n_rays, a.n_strat = N, spec["n_strat"]
         a.rays_o, a.rays_d = rays_o.data_ptr(), rays_d.data_ptr()
         for k, row in enumerate(spec["bound"]):
@@ -157,7 +157,7 @@ class ImapEvalFn(torch.autograd.Function):
         P = pts.shape[0]
         a = L.NcImapPointsArgs()
         a.abi_version = L.NC_ABI_VERSION
-        a.flags = L.NC_SAVE_FOR_BACKWARD if (torch.is_grad_enabled() and any(ctx.needs_input_grad)) else 0
+        a.flags = L.NC_SAVE_FOR_BACKWARD if any(ctx.needs_input_grad) else 0
         a.n_points, a.pts = P, pts.data_ptr()
         _fill_params(a.dec, params, device)
         raw = torch.empty(P, 4, device=device, dtype=torch.float32)
