@@ -23,7 +23,11 @@
 
 namespace nc {
 
-constexpr int GT_M = 64, GT_N = 64, GT_K = 16;  // workgroup tile (4 waves x 32 x 32)
+#ifndef NC_IMAP_GT_K
+#define NC_IMAP_GT_K 32
+#endif
+constexpr int GT_M = 64, GT_N = 64, GT_K = NC_IMAP_GT_K;  // workgroup tile (4 waves x 32 x 32), k-slice
+static_assert(GT_K % 16 == 0 && GT_K <= 64, "k-slice: whole 16-float rows per thread group");
 constexpr int GT_LD = GT_M + 4;                 // LDS row pad
 
 // C[m][n] (+)= sum_k A(m,k) B(k,n)
@@ -43,15 +47,15 @@ __global__ void __launch_bounds__(256) k_imap_gemm(const ImapGemm g) {
   floatx4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
   for (int64_t k0 = kb; k0 < ke; k0 += GT_K) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // 1024 elements of each operand tile, 4 per thread
+    for (int j = 0; j < GT_K / 4; ++j) {  // 64 x GT_K elements of each operand tile, GT_K / 4 per thread
       int kk, mm;
-      if (A_KM) { mm = t & 63; kk = (t >> 6) + 4 * j; } else { kk = t & 15; mm = (t >> 4) + 16 * j; }
+      if (A_KM) { mm = t & 63; kk = (t >> 6) + 4 * j; } else { kk = t % GT_K; mm = t / GT_K + (256 / GT_K) * j; }
       const int64_t gk = k0 + kk, gm = m0 + mm;
       float v = 0.f;
       if (gk < ke && gm < g.M) v = A_KM ? g.A[gk * g.lda + gm] : g.A[gm * g.lda + gk];
       As[kk][mm] = v;
       int kn, nn;
-      if (B_KN) { nn = t & 63; kn = (t >> 6) + 4 * j; } else { kn = t & 15; nn = (t >> 4) + 16 * j; }
+      if (B_KN) { nn = t & 63; kn = (t >> 6) + 4 * j; } else { kn = t % GT_K; nn = t / GT_K + (256 / GT_K) * j; }
       const int64_t hk = k0 + kn, hn = n0 + nn;
       float w = 0.f;
       if (hk < ke && hn < g.N) w = B_KN ? g.B[hk * g.ldb + hn] : g.B[hn * g.ldb + hk];

@@ -106,11 +106,25 @@ def test_imap_tracker_mode_rays_only():
     assert all(p.grad is None for p in m.parameters())
 
 
+def _f64_truth(fn):
+    """fn(prm, dtype) under the oracle's float64 mode: the ground truth that both fp32
+    implementations are scored against (the Fourier arguments reach |x| ~ 1e2..1e3 rad,
+    so cos(x) in fp32 alone carries ~1e-5 relative error into the point gradients)."""
+    from oracle import nice_oracle as NO
+    with NO.float64_mode():
+        return fn(torch.float64)
+
+
+def _within(got, ref32, truth, name, floor=2e-5):
+    e_hip, e_ref = rel(got, truth), rel(ref32, truth)
+    assert e_hip <= max(4 * e_ref, floor), f"{name}: HIP {e_hip:.3g} vs fp32 reference {e_ref:.3g}"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("P", [1, 77, 20000])
 def test_imap_points_forward_backward_vs_oracle(P):
     """MLP.forward(p) on caller points (ragged sizes, tile tails) and its backward vs autograd
-    through the oracle."""
+    through the oracle (fp32, and float64 as ground truth)."""
     bound, params = _scene()
     g = torch.Generator().manual_seed(P)
     p = (torch.rand(P, 3, generator=g, dtype=torch.float64) * 1.2 - 0.1)
@@ -119,19 +133,26 @@ def test_imap_points_forward_backward_vs_oracle(P):
     raw = m(pg)
     up = torch.randn(P, 4, generator=g)
     raw.backward(up.cuda())
-    prm = {k: v.clone().requires_grad_(True) for k, v in params.items()}
-    pc = p.clone().requires_grad_(True)
-    ref = IO.imap_forward(pc, prm)
-    ref.backward(up)
+
+    def run(dtype):
+        prm = {k: v.to(dtype).clone().requires_grad_(True) for k, v in params.items()}
+        pc = p.clone().requires_grad_(True)
+        out = IO.imap_forward(pc, prm)
+        out.backward(up.to(dtype))
+        return out, pc.grad, prm
+
+    ref, ref_gp, ref_prm = run(torch.float32)
+    tru, tru_gp, tru_prm = _f64_truth(run)
     assert rel(raw, ref) <= OUT_TOL
-    assert rel(pg.grad, pc.grad) <= GRAD_TOL
+    _within(pg.grad, ref_gp, tru_gp, "points")
     for n, q in m.named_parameters():
-        assert rel(q.grad, prm[n].grad) <= GRAD_TOL, n
+        _within(q.grad, ref_prm[n].grad, tru_prm[n].grad, n)
 
 
 @pytest.mark.gpu
 def test_imap_bench_size_vs_oracle():
-    """1,000 rays x (32 + 12 importance) samples on the room0 bound: HIP vs the CPU oracle."""
+    """1,000 rays x (32 + 12 importance) samples on the room0 bound: HIP vs the CPU oracle
+    (outputs at 1e-4 of the fp32 oracle; gradients against the float64 ground truth)."""
     from nicecore import scene as S
     sc = S.make_scene("replica_room0")
     bound, params = sc.bound, _scene()[1]
@@ -141,14 +162,21 @@ def test_imap_bench_size_vs_oracle():
     rog, rdg = ro.cuda().requires_grad_(True), rd.cuda().requires_grad_(True)
     d, v, c = r.render_batch_ray(None, m, rdg, rog, "cuda", "color", dep.cuda())
     (d.sum() + c.sum()).backward()
-    prm = {k: x.clone().requires_grad_(True) for k, x in params.items()}
-    roc, rdc = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
-    dc, vc, cc = IO.render_batch_ray(prm, bound, rdc, roc, dep, 32, 12)
-    (dc.sum() + cc.sum()).backward()
+
+    def run(dtype):
+        prm = {k: x.to(dtype).clone().requires_grad_(True) for k, x in params.items()}
+        roc, rdc = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
+        dc, vc, cc = IO.render_batch_ray(prm, bound, rdc, roc, dep, 32, 12)
+        (dc.sum() + cc.sum()).backward()
+        return dc, cc, roc.grad, rdc.grad, prm
+
+    dc, cc, gro, grd, prm = run(torch.float32)
     assert rel(d, dc) <= 1e-4 and rel(c, cc) <= 1e-4
-    assert rel(rog.grad, roc.grad) <= 1e-3
+    _, _, tgro, tgrd, tprm = _f64_truth(run)
+    _within(rog.grad, gro, tgro, "rays_o", floor=1e-4)
+    _within(rdg.grad, grd, tgrd, "rays_d", floor=1e-4)
     for n, q in m.named_parameters():
-        assert rel(q.grad, prm[n].grad) <= 1e-3, n
+        _within(q.grad, prm[n].grad, tprm[n].grad, n, floor=1e-4)
 
 
 @pytest.mark.gpu
