@@ -24,7 +24,7 @@
 namespace nc {
 
 #ifndef NC_IMAP_GT_K
-#define NC_IMAP_GT_K 32
+#define NC_IMAP_GT_K 16
 #endif
 constexpr int GT_M = 64, GT_N = 64, GT_K = NC_IMAP_GT_K;  // workgroup tile (4 waves x 32 x 32), k-slice
 static_assert(GT_K % 16 == 0 && GT_K <= 64, "k-slice: whole 16-float rows per thread group");
@@ -34,6 +34,20 @@ constexpr int GT_LD = GT_M + 4;                 // LDS row pad
 //   A_KM: A(m,k) = A[k*lda + m]   else A[m*lda + k]
 //   B_KN: B(k,n) = B[k*ldb + n]   else B[n*ldb + k]
 // epilogue: + bias[n]; relu; * (mask[m*ldm + n] > 0); atomic accumulate (split-K).
+// one k-slice of the wave's 32 x 32 sub-tile: 2 x 2 blocks of v_mfma_f32_16x16x4_f32
+__device__ __forceinline__ void slice_mfma(const float (&As)[GT_K][GT_LD], const float (&Bs)[GT_K][GT_LD], int wm,
+                                           int wn, int i, int q, floatx4 (&acc)[2][2]) {
+#pragma unroll
+  for (int kk = 0; kk < GT_K; kk += 4) {
+    const float a0 = As[kk + q][wm + i], a1 = As[kk + q][wm + 16 + i];
+    const float b0 = Bs[kk + q][wn + i], b1 = Bs[kk + q][wn + 16 + i];
+    acc[0][0] = mfma4(a0, b0, acc[0][0]);
+    acc[0][1] = mfma4(a0, b1, acc[0][1]);
+    acc[1][0] = mfma4(a1, b0, acc[1][0]);
+    acc[1][1] = mfma4(a1, b1, acc[1][1]);
+  }
+}
+
 template <bool A_KM, bool B_KN>
 __global__ void __launch_bounds__(256) k_imap_gemm(const ImapGemm g) {
   __shared__ float As[GT_K][GT_LD];
@@ -62,15 +76,7 @@ __global__ void __launch_bounds__(256) k_imap_gemm(const ImapGemm g) {
       Bs[kn][nn] = w;
     }
     __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < GT_K; kk += 4) {
-      const float a0 = As[kk + q][wm + i], a1 = As[kk + q][wm + 16 + i];
-      const float b0 = Bs[kk + q][wn + i], b1 = Bs[kk + q][wn + 16 + i];
-      acc[0][0] = mfma4(a0, b0, acc[0][0]);
-      acc[0][1] = mfma4(a0, b1, acc[0][1]);
-      acc[1][0] = mfma4(a1, b0, acc[1][0]);
-      acc[1][1] = mfma4(a1, b1, acc[1][1]);
-    }
+    slice_mfma(As, Bs, wm, wn, i, q, acc);
     __syncthreads();
   }
   // D layout: register r of lane (i, q) = C[row 4q + r][col i] of the 16x16 block
@@ -105,7 +111,7 @@ __global__ void k_imap_embed(const float4* pf, const float* B, int64_t P, float*
   if (j < EMB) {
     const float4 f = pf[p];
     const float x = __builtin_fmaf(f.z, B[2 * EMB + j], __builtin_fmaf(f.y, B[EMB + j], f.x * B[j]));
-    v = fourier_sin(x);
+    v = sinf(x);  // ocml (6.8e-8 abs): |x| <= ~3e2 here; the decoder is 14x the MACs of a NICE MLP
   }
   emb[e] = v;
 }
@@ -120,7 +126,7 @@ __global__ void k_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, 
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
   for (int j = 0; j < EMB; ++j) {
     const float x = __builtin_fmaf(f.z, B[2 * EMB + j], __builtin_fmaf(f.y, B[EMB + j], f.x * B[j]));
-    const float v = demb[p * EMBP + j] * fourier_cos(x);
+    const float v = demb[p * EMBP + j] * cosf(x);
     if (dx) dx[p * EMBP + j] = v;
     d0 = d0 + B[j] * v;
     d1 = d1 + B[EMB + j] * v;
