@@ -26,25 +26,35 @@ namespace nc {
 #ifndef NC_IMAP_GT_K
 #define NC_IMAP_GT_K 16
 #endif
-constexpr int GT_M = 64, GT_N = 64, GT_K = NC_IMAP_GT_K;  // workgroup tile (4 waves x 32 x 32), k-slice
+#ifndef NC_IMAP_WT
+#define NC_IMAP_WT 2
+#endif
+// workgroup tile: 2 x 2 waves, each WT x WT blocks of 16 x 16; k-slice GT_K
+constexpr int WT = NC_IMAP_WT;
+constexpr int GT_M = 32 * WT, GT_N = 32 * WT, GT_K = NC_IMAP_GT_K;
 static_assert(GT_K % 16 == 0 && GT_K <= 64, "k-slice: whole 16-float rows per thread group");
+static_assert(GT_M * GT_K % 256 == 0 && GT_M <= 256, "operand tile loads: whole elements per thread");
 constexpr int GT_LD = GT_M + 4;                 // LDS row pad
 
 // C[m][n] (+)= sum_k A(m,k) B(k,n)
 //   A_KM: A(m,k) = A[k*lda + m]   else A[m*lda + k]
 //   B_KN: B(k,n) = B[k*ldb + n]   else B[n*ldb + k]
 // epilogue: + bias[n]; relu; * (mask[m*ldm + n] > 0); atomic accumulate (split-K).
-// one k-slice of the wave's 32 x 32 sub-tile: 2 x 2 blocks of v_mfma_f32_16x16x4_f32
+// one k-slice of the wave's (16 WT) x (16 WT) sub-tile: WT x WT blocks of v_mfma_f32_16x16x4_f32
 __device__ __forceinline__ void slice_mfma(const float (&As)[GT_K][GT_LD], const float (&Bs)[GT_K][GT_LD], int wm,
-                                           int wn, int i, int q, floatx4 (&acc)[2][2]) {
+                                           int wn, int i, int q, floatx4 (&acc)[WT][WT]) {
 #pragma unroll
   for (int kk = 0; kk < GT_K; kk += 4) {
-    const float a0 = As[kk + q][wm + i], a1 = As[kk + q][wm + 16 + i];
-    const float b0 = Bs[kk + q][wn + i], b1 = Bs[kk + q][wn + 16 + i];
-    acc[0][0] = mfma4(a0, b0, acc[0][0]);
-    acc[0][1] = mfma4(a0, b1, acc[0][1]);
-    acc[1][0] = mfma4(a1, b0, acc[1][0]);
-    acc[1][1] = mfma4(a1, b1, acc[1][1]);
+    float a[WT], b[WT];
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+      a[u] = As[kk + q][wm + 16 * u + i];
+      b[u] = Bs[kk + q][wn + 16 * u + i];
+    }
+#pragma unroll
+    for (int bm = 0; bm < WT; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < WT; ++bn) acc[bm][bn] = mfma4(a[bm], b[bn], acc[bm][bn]);
   }
 }
 
@@ -57,19 +67,23 @@ __global__ void __launch_bounds__(256) k_imap_gemm(const ImapGemm g) {
   const int64_t n0 = (int64_t)blockIdx.y * GT_N;
   const int64_t kb = (int64_t)blockIdx.z * g.k_split;
   const int64_t ke = kb + g.k_split < g.K ? kb + g.k_split : g.K;
-  const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
-  floatx4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
+  const int wm = (wave & 1) * 16 * WT, wn = (wave >> 1) * 16 * WT;
+  floatx4 acc[WT][WT];
+#pragma unroll
+  for (int bm = 0; bm < WT; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < WT; ++bn) acc[bm][bn] = zero4();
   for (int64_t k0 = kb; k0 < ke; k0 += GT_K) {
 #pragma unroll
-    for (int j = 0; j < GT_K / 4; ++j) {  // 64 x GT_K elements of each operand tile, GT_K / 4 per thread
+    for (int j = 0; j < GT_M * GT_K / 256; ++j) {  // GT_M x GT_K elements of each operand tile
       int kk, mm;
-      if (A_KM) { mm = t & 63; kk = (t >> 6) + 4 * j; } else { kk = t % GT_K; mm = t / GT_K + (256 / GT_K) * j; }
+      if (A_KM) { mm = t % GT_M; kk = t / GT_M + (256 / GT_M) * j; } else { kk = t % GT_K; mm = t / GT_K + (256 / GT_K) * j; }
       const int64_t gk = k0 + kk, gm = m0 + mm;
       float v = 0.f;
       if (gk < ke && gm < g.M) v = A_KM ? g.A[gk * g.lda + gm] : g.A[gm * g.lda + gk];
       As[kk][mm] = v;
       int kn, nn;
-      if (B_KN) { nn = t & 63; kn = (t >> 6) + 4 * j; } else { kn = t % GT_K; nn = t / GT_K + (256 / GT_K) * j; }
+      if (B_KN) { nn = t % GT_N; kn = t / GT_N + (256 / GT_N) * j; } else { kn = t % GT_K; nn = t / GT_K + (256 / GT_K) * j; }
       const int64_t hk = k0 + kn, hn = n0 + nn;
       float w = 0.f;
       if (hk < ke && hn < g.N) w = B_KN ? g.B[hk * g.ldb + hn] : g.B[hn * g.ldb + hk];
@@ -81,9 +95,9 @@ __global__ void __launch_bounds__(256) k_imap_gemm(const ImapGemm g) {
   }
   // D layout: register r of lane (i, q) = C[row 4q + r][col i] of the 16x16 block
 #pragma unroll
-  for (int bm = 0; bm < 2; ++bm) {
+  for (int bm = 0; bm < WT; ++bm) {
 #pragma unroll
-    for (int bn = 0; bn < 2; ++bn) {
+    for (int bn = 0; bn < WT; ++bn) {
       const int64_t n = n0 + wn + 16 * bn + i;
       if (n >= g.N) continue;
       const float bias = g.bias ? g.bias[n] : 0.f;
