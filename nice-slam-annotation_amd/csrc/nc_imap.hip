@@ -131,42 +131,50 @@ __global__ void k_imap_embed(const float4* pf, const float* B, int64_t P, float*
 }
 
 // dx[p][j] = demb[p][j] * cos(x_j) (stored for dB = pf^T dx) and d p.float() = B dx
-// -> dpts (float64, the .float() cast's backward).  Thread = point.
-__global__ void k_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, const float* demb, float* dx,
-                                   double* dpts) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  const float4 f = pf[p];
-  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-  for (int j = 0; j < EMB; ++j) {
+// -> dpts (float64, the .float() cast's backward).  Block = 2 points x 96 features
+// (coalesced row reads), the 3 x 96 products of a point summed through LDS.
+constexpr int FB_PTS = 2;
+__global__ void __launch_bounds__(FB_PTS * EMBP) k_imap_fourier_bwd(const float4* pf, const float* B, int64_t P,
+                                                                     const float* demb, float* dx, double* dpts) {
+  __shared__ float red[3][FB_PTS * EMBP];
+  const int t = threadIdx.x, lp = t / EMBP, j = t - lp * EMBP;
+  const int64_t p = (int64_t)blockIdx.x * FB_PTS + lp;
+  float v = 0.f;
+  if (p < P && j < EMB) {
+    const float4 f = pf[p];
     const float x = __builtin_fmaf(f.z, B[2 * EMB + j], __builtin_fmaf(f.y, B[EMB + j], f.x * B[j]));
-    const float v = demb[p * EMBP + j] * cosf(x);
-    if (dx) dx[p * EMBP + j] = v;
-    d0 = d0 + B[j] * v;
-    d1 = d1 + B[EMB + j] * v;
-    d2 = d2 + B[2 * EMB + j] * v;
+    v = demb[p * EMBP + j] * cosf(x);
   }
-  if (dx) {
-#pragma unroll
-    for (int j = EMB; j < EMBP; ++j) dx[p * EMBP + j] = 0.f;
-  }
-  if (dpts) {
-    dpts[p * 3 + 0] = (double)d0;
-    dpts[p * 3 + 1] = (double)d1;
-    dpts[p * 3 + 2] = (double)d2;
+  if (dx && p < P) dx[p * EMBP + j] = v;  // pad columns 93..95 = 0
+  red[0][t] = j < EMB ? B[j] * v : 0.f;
+  red[1][t] = j < EMB ? B[EMB + j] * v : 0.f;
+  red[2][t] = j < EMB ? B[2 * EMB + j] * v : 0.f;
+  __syncthreads();
+  if (j < 3 && p < P && dpts) {
+    const float* r = red[j] + lp * EMBP;
+    float s = 0.f;
+    for (int k = 0; k < EMB; ++k) s = s + r[k];
+    dpts[p * 3 + j] = (double)s;
   }
 }
 
-// out[c] += sum_p X[p*ld + c] (bias gradients); block = 256 columns x one point slice
+// out[c] += sum_p X[p*ld + c] (bias gradients); block = one point slice, thread =
+// (column c = t % ncols, row phase t / ncols): 256 / ncols points in flight per step
 __global__ void __launch_bounds__(256) k_imap_colsum(const float* X, int64_t P, int ld, int ncols, int64_t per,
                                                      float* out) {
-  const int c = threadIdx.x;
-  if (c >= ncols) return;
+  const int rows = 256 / ncols;
+  const int c = threadIdx.x % ncols, r = threadIdx.x / ncols;
+  if (r >= rows) return;
   const int64_t pb = (int64_t)blockIdx.x * per;
   const int64_t pe = pb + per < P ? pb + per : P;
-  float s = 0.f;
-  for (int64_t p = pb; p < pe; ++p) s = s + X[p * ld + c];
-  atomicAdd(out + c, s);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
+  int64_t p = pb + r;
+  for (; p + 7 * rows < pe; p += 8 * rows) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] = s[u] + X[(p + u * rows) * ld + c];
+  }
+  for (; p < pe; p += rows) s[0] = s[0] + X[p * ld + c];
+  atomicAdd(out + c, ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
 }
 
 // raw [P][4] -> occupancy slot / rgb (RayCtx inputs of k_composite_*)
@@ -229,7 +237,8 @@ int launch_imap_embed(const float4* pf, const float* B, int64_t P, float* emb, h
 int launch_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, const float* demb, float* dx, double* dpts,
                             hipStream_t s) {
   if (P <= 0) return 0;
-  hipLaunchKernelGGL(k_imap_fourier_bwd, dim3(blocks_of(P, 256)), dim3(256), 0, s, pf, B, P, demb, dx, dpts);
+  hipLaunchKernelGGL(k_imap_fourier_bwd, dim3(blocks_of(P, FB_PTS)), dim3(FB_PTS * EMBP), 0, s, pf, B, P, demb, dx,
+                     dpts);
   return (int)hipGetLastError();
 }
 

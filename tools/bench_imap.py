@@ -55,8 +55,9 @@ def main():
         rog = ro.requires_grad_(tracker)
         rdg = rd.requires_grad_(tracker)
         d, v, c = r.render_batch_ray(None, m, rdg, rog, "cuda", "color", dep)
-        mask = dep > 0
-        loss = (dep[mask] - d[mask]).abs().sum() + w_col * (col - c).abs().sum()
+        # Mapper.py:603-612 / Tracker.py:117-131 L1 terms; the depth mask as a where (no
+        # boolean-index host sync inside the timed step)
+        loss = torch.where(dep > 0, (dep - d).abs(), 0.).sum() + w_col * (col - c).abs().sum()
         loss.backward()
         for p in m.parameters():
             p.grad = None
