@@ -158,23 +158,35 @@ __global__ void __launch_bounds__(FB_PTS * EMBP) k_imap_fourier_bwd(const float4
   }
 }
 
-// out[c] += sum_p X[p*ld + c] (bias gradients); block = one point slice, thread =
-// (column c = t % ncols, row phase t / ncols): 256 / ncols points in flight per step
+// out[c] += sum_p X[p*ld + c] (bias gradients).  Block = (up to 64 columns) x (256 / that
+// rows) over one point slice; rows summed in LDS, then ONE atomic per column per block
+// (same-address atomics serialise in L2: slices, not blocks x rows, set their count).
+constexpr int CS_SLICES = 256;
 __global__ void __launch_bounds__(256) k_imap_colsum(const float* X, int64_t P, int ld, int ncols, int64_t per,
                                                      float* out) {
-  const int rows = 256 / ncols;
-  const int c = threadIdx.x % ncols, r = threadIdx.x / ncols;
-  if (r >= rows) return;
-  const int64_t pb = (int64_t)blockIdx.x * per;
+  __shared__ float part[256];
+  const int cb = ncols < 64 ? ncols : 64, rows = 256 / cb;
+  const int cl = threadIdx.x % cb, r = threadIdx.x / cb;
+  const int c = blockIdx.x * cb + cl;
+  const bool on = r < rows && c < ncols;
+  const int64_t pb = (int64_t)blockIdx.y * per;
   const int64_t pe = pb + per < P ? pb + per : P;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
-  int64_t p = pb + r;
-  for (; p + 7 * rows < pe; p += 8 * rows) {
+  if (on) {
+    int64_t p = pb + r;
+    for (; p + 7 * rows < pe; p += 8 * rows) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s[u] = s[u] + X[(p + u * rows) * ld + c];
+      for (int u = 0; u < 8; ++u) s[u] = s[u] + X[(p + u * rows) * ld + c];
+    }
+    for (; p < pe; p += rows) s[0] = s[0] + X[p * ld + c];
   }
-  for (; p < pe; p += rows) s[0] = s[0] + X[p * ld + c];
-  atomicAdd(out + c, ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
+  part[threadIdx.x] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (r == 0 && c < ncols) {
+    float t = 0.f;
+    for (int k = 0; k < rows; ++k) t = t + part[k * cb + cl];
+    atomicAdd(out + c, t);
+  }
 }
 
 // raw [P][4] -> occupancy slot / rgb (RayCtx inputs of k_composite_*)
@@ -244,10 +256,13 @@ int launch_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, const f
 
 int launch_imap_colsum(const float* X, int64_t P, int ld, int ncols, float* out, hipStream_t s) {
   if (P <= 0) return 0;
-  int64_t slices = (P + 255) / 256;
-  if (slices > 1024) slices = 1024;
+  if (ncols < 1 || ncols > 256) return (int)hipErrorInvalidValue;
+  int64_t slices = (P + 1023) / 1024;
+  if (slices > CS_SLICES) slices = CS_SLICES;
   const int64_t per = (P + slices - 1) / slices;
-  hipLaunchKernelGGL(k_imap_colsum, dim3(blocks_of(P, (int)per)), dim3(256), 0, s, X, P, ld, ncols, per, out);
+  const int cb = ncols < 64 ? ncols : 64;
+  const dim3 grid((unsigned)((ncols + cb - 1) / cb), (unsigned)((P + per - 1) / per));
+  hipLaunchKernelGGL(k_imap_colsum, grid, dim3(256), 0, s, X, P, ld, ncols, per, out);
   return (int)hipGetLastError();
 }
 
