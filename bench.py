@@ -13,6 +13,10 @@ bound that render_batch_ray needs before sampling).  Weak scaling: every rank
 renders its own 1000 rays.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ba|tracker]
+
+--gpus N > 1 either runs under torch.distributed.run (WORLD_SIZE set: one rank of N) or,
+without a launcher, starts the N ranks itself (launch_ranks: torch.multiprocessing spawn,
+MASTER_ADDR 127.0.0.1, a free port).
 """
 from __future__ import annotations
 
@@ -93,10 +97,44 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned_rank(local, world, port, argv):
+    """Entry of one rank started by launch_ranks (a fresh interpreter: torch.multiprocessing
+    'spawn'), with the environment torch.distributed.run would have given it."""
+    os.environ.update(RANK=str(local), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.argv = argv
+    main()
+
+
+def launch_ranks(args) -> None:
+    """``python bench.py --gpus N`` without an external launcher: start N rank processes
+    (one per GPU) and wait for them.  The parent makes no HIP call (device_count() does
+    not initialise the runtime on this image), so no rank inherits a GPU context."""
+    import torch.multiprocessing as mp
+    n = args.gpus
+    have = torch.cuda.device_count()
+    if args.backend == "nccl" and n > have:
+        raise SystemExit(f"bench.py: --gpus {n} but only {have} HIP device(s) are visible "
+                         f"(RCCL needs one GPU per rank; --backend gloo rehearses N ranks on fewer GPUs)")
+    if have == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    mp.spawn(_spawned_rank, args=(n, _free_port(), list(sys.argv)), nprocs=n, join=True)
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     if world > 1:
         import torch.distributed as dist
         dev = local % torch.cuda.device_count()  # == local on a node with >= N GPUs
@@ -105,6 +143,8 @@ def setup_dist(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:  # rehearsal of the N>1 path with several ranks on one GPU
             dist.init_process_group(args.backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -449,6 +489,9 @@ def time_mapper_iteration(w, args):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args)  # rank 0 prints the JSON line
+        return
     world, rank, local = setup_dist(args)
     device = torch.device("cuda", torch.cuda.current_device())
     from nicecore import _lib as L

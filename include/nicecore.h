@@ -76,7 +76,7 @@ extern "C" {
  * called later on the same workspace.  Lets a data-parallel caller start the grid-
  * gradient all-reduce while the weight gradients are still being computed. */
 #define NC_DEFER_PARAM_GRADS 8
-/* nc_render_forward / _backward (ABI v7, additive): the backward will not ask for decoder
+/* nc_render_forward / _backward (ABI v8, additive): the backward will not ask for decoder
  * `kind`'s weight gradient (its parameters do not require grad: the Tracker's frozen
  * decoders, the Mapper's fix_fine).  The forward then skips that decoder's per-point
  * activation records (5 x 32 floats per point), which only k_mlp_dw reads; a backward

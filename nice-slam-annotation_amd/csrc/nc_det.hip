@@ -81,17 +81,22 @@ __device__ __forceinline__ uint64_t shfl_key(uint64_t v, int src) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// the summed run of voxel key k0 into its gradient row.  Plain stores: every voxel of a
-// grid is the key of at most one run (each grid belongs to one job: a decoder samples
-// its own grid with grad, Plan), the run has one writer, and the row was zeroed
-// before the backward (the gather's grad_zero fill, or k_rows_compact for sparse rows)
+// the summed run of voxel key k0 added to its gradient row.  Read-add-write without an
+// atomic: every voxel of a grid is the key of at most one run (each grid belongs to one
+// job: a decoder samples its own grid with grad, Plan), so the run has one writer.  The
+// add (not a store) keeps the accumulate contract of nicecore.h: sparse rows collect
+// several forward/backward calls until nc_sparse_rows_clear, and a caller's dense
+// gradient buffer keeps what was in it, exactly as the float-atomic path does
 __device__ __forceinline__ void det_add(const MlpCtx& m, const DetBufs& d, uint64_t k0, int ch, float acc) {
   const int j = (int)(k0 >> d.vbits);
   const uint64_t v = k0 & ((uint64_t(1) << d.vbits) - 1);
   const nc_grid G = grid_of(m, job_of(m, j).kind);
   if (G.grad_rows) {  // sparse gradient rows (claimed by the forward)
     const int r = G.grad_rows[v];
-    if (r >= 0) G.grad[(int64_t)r * 32 + ch] = acc;
+    if (r >= 0) {
+      float* dst = G.grad + (int64_t)r * 32 + ch;
+      *dst = *dst + acc;
+    }
     return;
   }
   const int64_t H = G.dims[1], W = G.dims[2];
@@ -102,7 +107,7 @@ __device__ __forceinline__ void det_add(const MlpCtx& m, const DetBufs& d, uint6
     const int64_t x = (int64_t)(v % W), y = (int64_t)((v / W) % H), z = (int64_t)(v / (W * H));
     dst = G.grad + z * G.grad_stride[1] + y * G.grad_stride[2] + x * G.grad_stride[3] + (int64_t)ch * G.grad_stride[0];
   }
-  *dst = acc;
+  *dst = *dst + acc;
 }
 
 // half-wave = sub-chunk s (entries [32 s, 32 s + 32)), lane = channel.  The run sums are

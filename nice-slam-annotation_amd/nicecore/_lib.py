@@ -15,13 +15,15 @@ LIB_PATH = os.path.join(HERE, "libnicecore.so")
 NC_ABI_VERSION = 8
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
+NC_SAVE_POINT_JACOBIAN = 4
 NC_DEFER_PARAM_GRADS = 8
 
 
 def NC_NO_WEIGHT_GRAD(kind: int) -> int:
     """include/nicecore.h: the backward will not ask for decoder ``kind``'s weight gradient."""
     return 16 << kind
-NC_SAVE_POINT_JACOBIAN = 4
+
+
 NC_LOSS_NONE, NC_LOSS_MAPPER, NC_LOSS_TRACKER = 0, 1, 2
 NC_LOSS_COLOR, NC_LOSS_DYNAMIC = 1, 2
 NC_MAX_SAMPLES = 64

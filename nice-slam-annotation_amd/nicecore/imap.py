@@ -19,6 +19,19 @@ import torch
 from . import _lib as L
 
 
+def _refuse_nondeterministic(needs_param_grad: bool) -> None:
+    """The iMAP* weight gradients are split-K float-atomic sums (csrc/nc_imap.hip), so
+    their rounding differs from run to run.  A caller that asked for deterministic
+    results (NC_DETERMINISTIC=1 or torch.use_deterministic_algorithms(True), as the NICE
+    path honours them) gets an error instead of silently varying gradients, the way
+    PyTorch refuses its own nondeterministic kernels in that mode."""
+    from .render_fn import deterministic_requested
+    if needs_param_grad and deterministic_requested():
+        raise L.NiceCoreError("nicecore: the iMAP* path has no deterministic weight-gradient reduction "
+                              "(split-K float atomics); unset NC_DETERMINISTIC / "
+                              "torch.use_deterministic_algorithms or freeze the MLP parameters")
+
+
 def imap_params(module) -> list:
     """The iMAP* MLP's parameters in ``parameters()`` order (embedder._B,
     pts_linears[0..3].weight/bias, output_linear.weight/bias), checked against the
@@ -67,6 +80,7 @@ class ImapRenderFn(torch.autograd.Function):
         if device.type != "cuda":
             raise L.NiceCoreError("nicecore renders on a HIP device; tensors are on " + str(device))
         ctx.set_materialize_grads(False)
+        _refuse_nondeterministic(any(ctx.needs_input_grad[4:]))
         rays_o = rays_o.detach().float().contiguous()
         rays_d = rays_d.detach().float().contiguous()
         N = rays_o.shape[0]
@@ -153,6 +167,7 @@ class ImapEvalFn(torch.autograd.Function):
         device = p.device
         if device.type != "cuda":
             raise L.NiceCoreError("nicecore evaluates on a HIP device; points are on " + str(device))
+        _refuse_nondeterministic(any(ctx.needs_input_grad[1:]))
         pts = p.detach().reshape(-1, 3).double().contiguous()
         P = pts.shape[0]
         a = L.NcImapPointsArgs()

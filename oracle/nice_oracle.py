@@ -50,9 +50,74 @@ def normalize_3d_coordinate(p: torch.Tensor, bound: torch.Tensor) -> torch.Tenso
     return torch.stack(cols, dim=1)
 
 
-def sample_grid_feature(p: torch.Tensor, grid: torch.Tensor, bound: torch.Tensor) -> torch.Tensor:
+# Windowed grids (tests of the 26-GB C5 grids only): grid key -> (full [D, H, W], window
+# offset (z0, y0, x0)).  The grid tensor passed for such a key is a window
+# grid[:, :, z0:z0+d, y0:y0+h, x0:x0+w] of a grid too large for the CPU, and its lookups
+# are computed as F.grid_sample on the FULL grid would compute them (sample_grid_window).
+_WINDOWS: dict = {}
+
+
+@contextlib.contextmanager
+def grid_windows(spec: dict):
+    """Within the block, lookups of the grids named in ``spec`` use sample_grid_window."""
+    global _WINDOWS
+    old, _WINDOWS = _WINDOWS, dict(spec)
+    try:
+        yield
+    finally:
+        _WINDOWS = old
+
+
+def sample_grid_window(p, window, bound, full_dims, offset):
+    """F.grid_sample(grid, normalize(p), border, align_corners=True) of decoder.py:179-188
+    for a grid of which only ``window`` is held, restating ATen's grid_sampler_3d (CPU):
+    unnormalise on the FULL grid ix = ((x + 1) / 2) * (W - 1) in the compute dtype, clip
+    to [0, W - 1] (border; zero coordinate gradient where clipped or on a border), corners floor(ix) and
+    +1, weights tnw = (ix_bse - ix)(iy_bse - iy)(iz_bse - iz) ... bse, corners outside the
+    grid skipped, out = tnw·v_tnw + tne·v_tne + tsw + tse + bnw + bne + bsw + bse in that
+    order.  The window offset is subtracted from the integer corner indices only, so the
+    weights are those of the full grid, bit for bit.  A corner outside the window that is
+    inside the full grid raises (the caller sized the window too small).  Returns [P, C]."""
+    vn = normalize_3d_coordinate(p, bound).to(FLOAT)
+    D, H, W = full_dims
+    z0, y0, x0 = offset
+    d, h, w = window.shape[2:]
+    src = window[0].permute(1, 2, 3, 0)  # [d, h, w, C]
+
+    def unnorm(x, size):
+        # clip_coordinates_set_grad: the borders count as clipped (zero gradient at 0
+        # and at size - 1 exactly), unlike clamp's inclusive gradient
+        u = ((x + 1) / 2) * (size - 1)
+        keep = (u > 0) & (u < size - 1)
+        return torch.where(keep, u, u.detach().clamp(0, size - 1))
+
+    ix, iy, iz = unnorm(vn[:, 0], W), unnorm(vn[:, 1], H), unnorm(vn[:, 2], D)
+    fx, fy, fz = ix.detach().floor(), iy.detach().floor(), iz.detach().floor()
+    out = None
+    # ATen's corner order: t/b = z, n/s = y, w/e = x
+    for dz, dy, dx in ((0, 0, 0), (0, 0, 1), (0, 1, 0), (0, 1, 1), (1, 0, 0), (1, 0, 1), (1, 1, 0), (1, 1, 1)):
+        cx, cy, cz = fx + dx, fy + dy, fz + dz
+        # the weight of corner (dx, dy, dz) is built from the opposite corner's distances
+        wx = (ix - fx) if dx else ((fx + 1) - ix)
+        wy = (iy - fy) if dy else ((fy + 1) - iy)
+        wz = (iz - fz) if dz else ((fz + 1) - iz)
+        wgt = wx * wy * wz
+        inb = (cx < W) & (cy < H) & (cz < D)
+        lx, ly, lz = (cx - x0).long(), (cy - y0).long(), (cz - z0).long()
+        inw = (lx >= 0) & (lx < w) & (ly >= 0) & (ly < h) & (lz >= 0) & (lz < d)
+        if bool((inb & ~inw).any()):
+            raise ValueError("sample_grid_window: a lookup needs a voxel outside the window")
+        val = src[lz.clamp(0, d - 1), ly.clamp(0, h - 1), lx.clamp(0, w - 1)]  # [P, C]
+        term = val * torch.where(inb, wgt, torch.zeros_like(wgt))[:, None]
+        out = term if out is None else out + term
+    return out
+
+
+def sample_grid_feature(p: torch.Tensor, grid: torch.Tensor, bound: torch.Tensor, key: str = "") -> torch.Tensor:
     """decoder.py:179-188 — trilinear (mode 'bilinear' on 5-D), border padding,
     align_corners=True.  Returns [P, C]."""
+    if key in _WINDOWS:
+        return sample_grid_window(p, grid, bound, *_WINDOWS[key])
     vgrid = normalize_3d_coordinate(p, bound).unsqueeze(0)[:, :, None, None].to(FLOAT)
     c = F.grid_sample(grid, vgrid, padding_mode='border', align_corners=True, mode='bilinear')
     return c.squeeze(-1).squeeze(-1).transpose(1, 2).squeeze(0)
@@ -64,10 +129,10 @@ def _lin(x, prm, name):
 
 def mlp_forward(p, grids, prm, pre, name, bound, color=False, concat=False):
     """decoder.py:190-219 (MLP.forward, fourier embedding, skips=[2])."""
-    c = sample_grid_feature(p, grids['grid_' + name], bound)
+    c = sample_grid_feature(p, grids['grid_' + name], bound, 'grid_' + name)
     if concat:  # decoder.py:196-202: middle feature concatenated without grad
         with torch.no_grad():
-            c_mid = sample_grid_feature(p, grids['grid_middle'], bound)
+            c_mid = sample_grid_feature(p, grids['grid_middle'], bound, 'grid_middle')
         c = torch.cat([c, c_mid], dim=1)
     pf = p.to(FLOAT)
     emb = torch.sin(pf @ prm[pre + 'embedder._B'])  # decoder.py:26-30
@@ -83,7 +148,7 @@ def mlp_forward(p, grids, prm, pre, name, bound, color=False, concat=False):
 
 def mlp_no_xyz_forward(p, grids, prm, pre, bound):
     """decoder.py:285-297 (coarse decoder)."""
-    c = sample_grid_feature(p, grids['grid_coarse'], bound)
+    c = sample_grid_feature(p, grids['grid_coarse'], bound, 'grid_coarse')
     h = c
     for i in range(5):
         h = F.relu(_lin(h, prm, f'{pre}pts_linears.{i}'))

@@ -91,9 +91,10 @@ def compare(rec, got):
     return out
 
 
-def oracle_render_grads(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, f64=False):
+def oracle_render_grads(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, f64=False, depth_max=None):
     """CPU oracle render + backward; with f64=True everything runs in float64
-    (ground truth).  Returns {name: tensor} like run_case."""
+    (ground truth).  ``depth_max``: the batch-global max(gt_depth) of a sharded batch.
+    Returns {name: tensor} like run_case."""
     from oracle import nice_oracle as O
     cast = (lambda t: t.double()) if f64 else (lambda t: t)
     ro_c = cast(ro.clone()).requires_grad_(True)
@@ -103,7 +104,8 @@ def oracle_render_grads(grids, params, dec_b, bound, ro, rd, stage, gt, upstream
     gt_c = cast(gt) if gt is not None else None
     ctx = O.float64_mode() if f64 else _null()
     with ctx:
-        d, v, c = O.render_batch_ray(g_c, prm_c, dec_b, bound, rd_c, ro_c, stage, gt_c)
+        dm = None if depth_max is None else cast(depth_max.reshape(()).clone())
+        d, v, c = O.render_batch_ray(g_c, prm_c, dec_b, bound, rd_c, ro_c, stage, gt_c, depth_max=dm)
         gd, gv, gc = upstream
         torch.autograd.backward([d, v, c], [gd, gv, cast(gc)])
     out = {"depth": d.detach(), "var": v.detach(), "color": c.detach(),
