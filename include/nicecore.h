@@ -499,6 +499,11 @@ int nc_imap_render_backward(const nc_imap_render_args* args, void* workspace, si
 size_t nc_imap_points_workspace_bytes(const nc_imap_points_args* args);
 int nc_imap_points_forward(const nc_imap_points_args* args, void* workspace, size_t workspace_bytes, void* stream);
 int nc_imap_points_backward(const nc_imap_points_args* args, void* workspace, size_t workspace_bytes, void* stream);
+/* Byte offset inside the workspace of the saved hidden activations h_layer = relu(z)
+ * (layer 0..3, [n_points][256] float32, point-major) that nc_imap_points_forward wrote:
+ * read-only introspection (the tests score weight gradients against a float64 truth
+ * evaluated on the same ReLU branches).  Returns -1 for a bad layer or arguments. */
+int64_t nc_imap_points_activation_offset(const nc_imap_points_args* args, int layer);
 
 #ifdef __cplusplus
 }

@@ -159,7 +159,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
+  size_t dmax = 0, rflag = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
          coef_d = 0, coef_c = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
          dtemp_bytes = 0,
          total = 0;
@@ -226,6 +226,7 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
     return o;
   };
   w.dmax = take(16);
+  w.rflag = take(4 * MAX_JOBS);  // MlpCtx::range_flag
   w.z = rays ? take((size_t)P * 8) : 0;
   w.pts = rays ? take((size_t)P * 24) : 0;
   w.xyz = take((size_t)pl.n_jobs * P * 16);
@@ -367,6 +368,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
     m.claim_cap = w.claim_cap;
   }
   m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
+  m.range_flag = at<uint32_t>(ws, w.rflag);
   m.jac = w.has_jac ? at<float>(ws, w.jac) : nullptr;
 }
 
@@ -466,6 +468,7 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
 
 void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, const Ws& w, int64_t P, int S) {
   std::memset(&c, 0, sizeof(c));
+  c.range_flag = at<uint32_t>(ws, w.rflag);
   c.N = a->n_rays;
   c.P = P;
   c.S = S;
@@ -1259,6 +1262,12 @@ int nc_imap_render_backward(const nc_imap_render_args* a, void* ws, size_t ws_by
   if (!need_coord) return 0;
   rc.n_jobs = 1;  // the decoder's point gradients (one slot)
   return check_hip(timed(KID_RAY_GRADS, s, [&] { return launch_ray_grads(rc, s); }), "k_ray_grads");
+}
+
+int64_t nc_imap_points_activation_offset(const nc_imap_points_args* a, int layer) {
+  ImapWs w;
+  if (layer < 0 || layer > 3 || imap_points_prepare(a, w)) return -1;
+  return (int64_t)(w.h + (size_t)layer * a->n_points * IH * 4);
 }
 
 size_t nc_imap_points_workspace_bytes(const nc_imap_points_args* a) {

@@ -180,6 +180,19 @@ __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
   }
 }
 
+// split8 that also folds max |x| into amax (one v_max_f32 with an |.| modifier per
+// value): the range guard of the split-f16 forward.  hi = f16 RTZ(x) and the residual
+// scaled by 2^11 stay finite and exact-enough only for |x| < 2^15 (RANGE_LIMIT); a tile
+// that saw a larger (or infinite) operand is recomputed on the exact-f32 MFMA path
+// (nc_mlp.hip k_mlp_fwd_exact).  NaN operands pass (fmaxf drops them) and stay NaN, as
+// in the reference's fp32 addmm.
+constexpr float RANGE_LIMIT = 32768.f;
+__device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo, float& amax) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(x[j]));
+  split8(x, hi, lo);
+}
+
 // f16 weight image of k_mlp_fwd.
 //   f32 part first (floats): biases BL [5][32], BC [NFC][32], output WO [4][32], BO [4],
 //   Fourier B FB [3][96]; then, from byte HB, the matrices of pts_linears 0..4 and

@@ -69,6 +69,9 @@ struct MlpCtx {
   int64_t claim_cap;         // entries per shard: (waves of a job / CLAIM_SHARDS + 1) * 64
   float* dfeat;              // NC_DETERMINISTIC: [n_jobs][P][32] d features of each job's own grid
                              // (k_mlp_dx stores them instead of scattering with atomics), else NULL
+  uint32_t* range_flag;      // [MAX_JOBS] split-f16 range guard: k_mlp_fwd sets job j's word when
+                             // an operand reached RANGE_LIMIT, k_mlp_fwd_exact then recomputes the
+                             // job in f32; zeroed by k_ray_setup / k_points_prep (NULL: no guard)
 };
 
 // NC_DETERMINISTIC grid-gradient scatter (nc_det.hip): every (job, point, corner)
@@ -127,6 +130,7 @@ struct RayCtx {
   const float* depth_max;  // device scalar (user override or computed into the workspace)
   int32_t dmax_local;      // k_ray_setup reduces max(gt_depth) itself, per workgroup (small N):
                            // no k_depth_max launch
+  uint32_t* range_flag;    // [MAX_JOBS] k_mlp_fwd's range flags, zeroed here (MlpCtx::range_flag)
   double bound[3][2];
   float t_strat[NC_MAX_SAMPLES];
   double t_surf[NC_MAX_SURF];

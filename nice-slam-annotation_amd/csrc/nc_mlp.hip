@@ -30,9 +30,6 @@
 
 // A/B build: -DNC_MFMA_F32 runs the forward decoder GEMMs on the exact-f32 MFMA
 // (v_mfma_f32_16x16x4_f32, the round-1 kernel) instead of split-f16.
-#ifdef NC_MFMA_F32
-#define NC_FWD_F32
-#endif
 
 #ifdef NC_ABL_NO_TRIG  // timing-only ablation: no trig at all
 #define NC_SIN(x) (x)
@@ -152,7 +149,7 @@ __device__ __forceinline__ int hpos(int m, int o, int c, int plane) {  // byte o
 }
 
 template <int KIND, int NT>
-__device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_params& P) {
+__device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_params& P, float& amax) {
   using N = Net<KIND>;
   using H = NetH<KIND>;
   constexpr int CDW = N::XYZ ? HID * N::CD : 1, CB = N::XYZ ? HID : 1, NB = N::XYZ ? 3 * EMB : 1;
@@ -200,6 +197,7 @@ __device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_param
       if (e < HID * in) {
         const int o = e / in, c = e - o * in, cp = lin ? N::pack_col(m, c) : c;
         const float v = regs.v[k];
+        amax = fmaxf(amax, fabsf(v));    // split-f16 range guard (RANGE_LIMIT)
         const _Float16 h = (_Float16)v;  // hi / scaled lo halves of one weight
         *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 0)) = h;
         *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 1)) = (_Float16)((v - (float)h) * SPLIT_SCALE);
@@ -519,7 +517,8 @@ struct WaveIn {
 
 template <int KIND, int T>
 __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, const WaveIn<KIND> (&R)[T],
-                                               float (&out)[T][4], float* const (&rec)[T], bool keep_h) {
+                                               float (&out)[T][4], float* const (&rec)[T], bool keep_h,
+                                               float& amax) {
   using N = Net<KIND>;
   using H = NetH<KIND>;
   constexpr int CB = N::CD / 32;
@@ -528,7 +527,7 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
 #pragma unroll
   for (int b = 0; b < CB; ++b)
 #pragma unroll
-    for (int t = 0; t < T; ++t) split8(R[t].c + 8 * b, ch[b][t], cl[b][t]);
+    for (int t = 0; t < T; ++t) split8(R[t].c + 8 * b, ch[b][t], cl[b][t], amax);
   half8 eh[3][T], el[3][T];  // Fourier features sin(p.float() @ B), XYZ decoders
   if constexpr (N::XYZ) {
     const float* B = F + H::FB;
@@ -603,7 +602,7 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
       }
       if (L < 4) mlo[t] |= bits << (8 * L);
       else mhi[t] = bits;
-      if (L < 4) split8(h[t], xh[t], xl[t]);
+      if (L < 4) split8(h[t], xh[t], xl[t], amax);
       if (L == 2) {
         h2h[t] = xh[t];
         h2l[t] = xl[t];
@@ -642,15 +641,20 @@ __device__ __forceinline__ Job pick_job(const Job (&jobs)[MAX_JOBS], unsigned y)
 // decoder.py:179-188, and the fine decoder's grid_middle lookup, :196-202: make_corners +
 // gather8, the same arithmetic as k_grid_gather) instead of read from cfeat, and the
 // backward's gradient buffer is zero-filled at the end of the workgroup's tiles.
-template <int KIND, bool FUSE>
-__device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float* lds, int64_t wg, int64_t nwg) {
+// F32: the decoder GEMMs on the exact-f32 MFMA (wave_forward, the f32 LDS image) instead of
+// split-f16 (wave_forward_h).  The split-f16 instantiation folds max |operand| of its
+// weights and activations into amax and, if any reaches RANGE_LIMIT (nc_device.h), sets
+// the job's range flag, so that k_mlp_fwd_exact recomputes the job on the F32 path.
+template <int KIND, bool FUSE, bool F32>
+__device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j, float* lds, int64_t wg,
+                                        int64_t nwg, bool zero_fill) {
   constexpr int T = FWD_TILES;
   constexpr int CQ = Net<KIND>::CD / 16;
-#ifdef NC_FWD_F32
-  load_weights<KIND, PADW_FWD, fwd_threads(FUSE)>(lds, ctx.dec[KIND]);
-#else
-  load_weights_h<KIND, fwd_threads(FUSE)>(reinterpret_cast<char*>(lds), ctx.dec[KIND]);
-#endif
+  float amax = 0.f;
+  if constexpr (F32)
+    load_weights<KIND, PADW_FWD, fwd_threads(FUSE)>(lds, ctx.dec[KIND]);
+  else
+    load_weights_h<KIND, fwd_threads(FUSE)>(reinterpret_cast<char*>(lds), ctx.dec[KIND], amax);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
   const int64_t per = 16 * waves * T;  // points per workgroup iteration
@@ -683,11 +687,7 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     // keep the (loop-invariant) LDS weight reads inside the loop: hoisting all of
     // them out of the persistent loop would need thousands of registers
     asm volatile("" ::: "memory");
-#ifdef NC_FWD_F32
-    WaveRegs<KIND> R[T];
-#else
-    WaveIn<KIND> R[T];
-#endif
+    std::conditional_t<F32, WaveRegs<KIND>, WaveIn<KIND>> R[T];
     float* rec[T];
     int64_t pt[T];
 #pragma unroll
@@ -726,11 +726,10 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
     }
     load_inputs(blk + nwg);
     float out[T][4];
-#ifdef NC_FWD_F32
-    wave_forward<KIND, T>(lds, i, g, R, out, rec, job.keep_h != 0);
-#else
-    wave_forward_h<KIND, T>(reinterpret_cast<const char*>(lds), i, g, R, out, rec, job.keep_h != 0);
-#endif
+    if constexpr (F32)
+      wave_forward<KIND, T>(lds, i, g, R, out, rec, job.keep_h != 0);
+    else
+      wave_forward_h<KIND, T>(reinterpret_cast<const char*>(lds), i, g, R, out, rec, job.keep_h != 0, amax);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const int64_t p = pt[t];
@@ -745,8 +744,11 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, float
       }
     }
   }
+  if constexpr (!F32) {  // out of the f16 range: the whole job is recomputed (rare; one store per lane)
+    if (!(amax < RANGE_LIMIT) && ctx.range_flag) ctx.range_flag[j] = 1u;
+  }
   if constexpr (FUSE) {  // the backward's gradient buffer (nc_render_args.grad_zero): stores last
-    if (ctx.zero_fill) {
+    if (zero_fill && ctx.zero_fill) {
       const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
       for (int64_t z = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; z < ctx.zero_n4; z += nthr)
         ctx.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
@@ -759,20 +761,45 @@ __device__ __forceinline__ int job_of_wg(const int32_t (&off)[MAX_JOBS + 1], int
   return (b >= off[1] ? 1 : 0) + (b >= off[2] ? 1 : 0);
 }
 
-template <bool FUSE>
-__global__ void __launch_bounds__(fwd_threads(FUSE)) k_mlp_fwd(const MlpCtx ctx) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+#ifdef NC_MFMA_F32
+constexpr bool FWD_F32 = true;   // A/B build: every forward on the exact-f32 MFMA
+#else
+constexpr bool FWD_F32 = false;
+#endif
+
+template <bool FUSE, bool F32, bool EXACT>
+__device__ __forceinline__ void fwd_kernel(const MlpCtx& ctx, float* lds) {
   const int b = blockIdx.x;
   const int j = job_of_wg(ctx.fwd_off, b);
+  if constexpr (EXACT) {  // k_mlp_fwd_exact: only the jobs whose split-f16 operands left the range
+    if (ctx.range_flag == nullptr || ctx.range_flag[j] == 0u) return;
+  }
   const Job job = pick_job(ctx.jobs, j);
   const int o0 = j == 0 ? ctx.fwd_off[0] : (j == 1 ? ctx.fwd_off[1] : ctx.fwd_off[2]);
   const int o1 = j == 0 ? ctx.fwd_off[1] : (j == 1 ? ctx.fwd_off[2] : ctx.fwd_off[3]);
   switch (job.kind) {
-    case K_COARSE: fwd_job<K_COARSE, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
-    case K_MID: fwd_job<K_MID, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
-    case K_FINE: fwd_job<K_FINE, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
-    default: fwd_job<K_COLOR, FUSE>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_COARSE: fwd_job<K_COARSE, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
+    case K_MID: fwd_job<K_MID, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
+    case K_FINE: fwd_job<K_FINE, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
+    default: fwd_job<K_COLOR, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
   }
+}
+
+template <bool FUSE>
+__global__ void __launch_bounds__(fwd_threads(FUSE)) k_mlp_fwd(const MlpCtx ctx) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  fwd_kernel<FUSE, FWD_F32, false>(ctx, lds);
+}
+
+// The range guard's second pass (decoder.py:209-216 in fp32 addmm semantics): right after
+// k_mlp_fwd, every workgroup reads its job's range flag and returns at once when it is
+// clear (the normal case: one load per workgroup); a flagged job is recomputed whole on
+// the exact-f32 MFMA -- outputs, activation records and fused grid features overwritten
+// with the f32 path's, which needs no range.  The gradient buffer fill is not repeated.
+template <bool FUSE>
+__global__ void __launch_bounds__(fwd_threads(FUSE)) k_mlp_fwd_exact(const MlpCtx ctx) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  fwd_kernel<FUSE, true, true>(ctx, lds);
 }
 
 // flat-parameter index of a dW tile element, or -1 (padding)
@@ -1300,20 +1327,20 @@ __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
 // launch wrappers / layout queries
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
-#ifdef NC_FWD_F32
-constexpr int FWD_LDS_FLOATS =
+constexpr int FWD_F32_LDS_FLOATS =
     cmax(cmax(Net<K_COARSE, PADW_FWD>::WEIGHTS, Net<K_MID, PADW_FWD>::WEIGHTS),
          cmax(Net<K_FINE, PADW_FWD>::WEIGHTS, Net<K_COLOR, PADW_FWD>::WEIGHTS));
-#else
 constexpr int FWD_LDS_FLOATS =
-    cmax(cmax(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), cmax(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4;
-#endif
+    FWD_F32 ? FWD_F32_LDS_FLOATS
+            : cmax(cmax(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), cmax(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4;
+static_assert(FWD_F32_LDS_FLOATS * 4 <= 160 * 1024, "f32 weight image LDS budget");
 constexpr int DW_LDS_FLOATS = cmax(cmax(DwLayout<K_COARSE>::TOTAL, DwLayout<K_MID>::TOTAL),
                                    cmax(DwLayout<K_FINE>::TOTAL, DwLayout<K_COLOR>::TOTAL));
 static_assert(FWD_LDS_FLOATS * 4 <= 160 * 1024, "weight image LDS budget");
 static_assert(DW_LDS_FLOATS * 4 <= 160 * 1024, "dW staging LDS budget");
 
 int mlp_fwd_lds_bytes() { return FWD_LDS_FLOATS * 4; }
+int mlp_fwd_exact_lds_bytes() { return FWD_F32_LDS_FLOATS * 4; }
 int mlp_dw_lds_bytes() { return DW_LDS_FLOATS * 4; }
 int64_t max_param_count() {
   return cmax(cmax((int)Net<K_COARSE>::NPARAM, (int)Net<K_MID>::NPARAM),
@@ -1384,7 +1411,7 @@ int decoder_macs(int kind) {  // SURVEY.md §8a a10-a11 (MAC per point)
 // features, the operand splits and the record stores cost about the same for the
 // three xyz decoders, the fine decoder's second feature block a little more
 int fwd_tile_cost(int kind) {
-#if defined(NC_FWD_F32)
+#if defined(NC_MFMA_F32)
   return decoder_macs(kind);
 #elif defined(NC_FWD_COST_MACS)
   return decoder_macs(kind);
@@ -1402,10 +1429,21 @@ int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
   if (attr != 0 && (attr = set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes()) |
                            set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes())) != 0)
     return attr;
+  static int attr_x = -1;
+  if (attr_x != 0 && (attr_x = set_lds(k_mlp_fwd_exact<false>, mlp_fwd_exact_lds_bytes()) |
+                               set_lds(k_mlp_fwd_exact<true>, mlp_fwd_exact_lds_bytes())) != 0)
+    return attr_x;
+  const dim3 grid(c.fwd_off[c.n_jobs]);
   if (c.fuse_gather)
-    hipLaunchKernelGGL(k_mlp_fwd<true>, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS_FUSED), mlp_fwd_lds_bytes(), s, c);
+    hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(FWD_THREADS_FUSED), mlp_fwd_lds_bytes(), s, c);
   else
-    hipLaunchKernelGGL(k_mlp_fwd<false>, dim3(c.fwd_off[c.n_jobs]), dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
+    hipLaunchKernelGGL(k_mlp_fwd<false>, grid, dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  if (FWD_F32 || c.range_flag == nullptr) return 0;
+  if (c.fuse_gather)
+    hipLaunchKernelGGL(k_mlp_fwd_exact<true>, grid, dim3(FWD_THREADS_FUSED), mlp_fwd_exact_lds_bytes(), s, c);
+  else
+    hipLaunchKernelGGL(k_mlp_fwd_exact<false>, grid, dim3(FWD_THREADS), mlp_fwd_exact_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 

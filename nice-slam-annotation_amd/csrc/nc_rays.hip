@@ -53,6 +53,7 @@ __device__ __forceinline__ double min_nan(double a, double b) { return (a < b ||
 __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x < MAX_JOBS && c.range_flag) c.range_flag[threadIdx.x] = 0u;  // for k_mlp_fwd
   float dmax_blk = 0.f;
   if (c.dmax_local) {  // torch.max(gt_depth) over the whole batch, by every workgroup (N small)
     __shared__ float red[RAY_WAVES];
@@ -156,6 +157,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
 // points mode (NICE.forward on caller points): the same per-point prologue
 __global__ void k_points_prep(const MlpCtx m, float4* xyz, float4* pf) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < MAX_JOBS && m.range_flag) m.range_flag[p] = 0u;  // for k_mlp_fwd
   if (p >= m.P) return;
   double pt[3];
 #pragma unroll

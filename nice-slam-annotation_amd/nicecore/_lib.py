@@ -179,6 +179,7 @@ EXPORTS = {
     "nc_imap_points_workspace_bytes": (c_size_t, [POINTER(NcImapPointsArgs)]),
     "nc_imap_points_forward": (c_int, [POINTER(NcImapPointsArgs), c_void_p, c_size_t, c_void_p]),
     "nc_imap_points_backward": (c_int, [POINTER(NcImapPointsArgs), c_void_p, c_size_t, c_void_p]),
+    "nc_imap_points_activation_offset": (c_int64, [POINTER(NcImapPointsArgs), c_int]),
     "nc_sparse_merge_temp_bytes": (c_size_t, [c_int64, c_int64]),
     "nc_sparse_rows_merge": (c_int, [POINTER(NcSparseRows), POINTER(NcSparseRows), c_void_p, c_void_p,
                                      c_int32, c_int64, c_void_p, c_size_t, c_void_p]),

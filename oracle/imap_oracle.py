@@ -23,13 +23,31 @@ import torch.nn.functional as F
 from oracle import nice_oracle as NO
 
 
-def imap_forward(p, prm):
-    """decoder.py:190-219 with c_dim = 0 (no grid feature, no skip): raw [P,4]."""
+def imap_forward(p, prm, masks=None):
+    """decoder.py:190-219 with c_dim = 0 (no grid feature, no skip): raw [P,4].
+    ``masks`` (tests only): per hidden layer a [P,256] bool tensor imposed in place of
+    relu's own branch, h = z * mask -- the same piecewise-linear function evaluated on
+    given ReLU branches (a float64 truth on the branches an fp32 evaluation took)."""
     emb = torch.sin(p.to(NO.FLOAT) @ prm['embedder._B'])  # decoder.py:26-30
     h = emb
     for i in range(4):
-        h = F.relu(F.linear(h, prm[f'pts_linears.{i}.weight'], prm[f'pts_linears.{i}.bias']))
+        z = F.linear(h, prm[f'pts_linears.{i}.weight'], prm[f'pts_linears.{i}.bias'])
+        h = F.relu(z) if masks is None else z * masks[i].to(z.dtype)
     return F.linear(h, prm['output_linear.weight'], prm['output_linear.bias'])
+
+
+def imap_relu_masks(p, prm):
+    """The ReLU branches (z > 0) of imap_forward's four hidden layers, [P,256] bool each, in
+    the current compute dtype (tests: how many (point, unit) branches an fp32 evaluation
+    takes differently from float64)."""
+    with torch.no_grad():
+        h = torch.sin(p.to(NO.FLOAT) @ prm['embedder._B'])
+        out = []
+        for i in range(4):
+            z = F.linear(h, prm[f'pts_linears.{i}.weight'], prm[f'pts_linears.{i}.bias'])
+            out.append(z > 0)
+            h = F.relu(z)
+    return out
 
 
 def eval_points(p, prm, bound):

@@ -121,45 +121,74 @@ def _within(got, ref32, truth, name, floor=2e-5):
 
 
 def _within_set(got, ref32, truth, floor=2e-5):
-    """Weight gradients: a ReLU whose pre-activation lies within fp32 rounding of 0 flips
-    its mask between any two fp32 evaluations, and with random-sign upstream gradients one
-    flipped (point, unit) moves a weight-gradient entry by ~1/sqrt(P) of the tensor's max:
-    which tensor a flip lands in is chance (measured on the CPU: the fp32 oracle's own
-    error vs float64 is 5e-7 on one layer and 1.9e-3 on the next at P = 20,000).  So each
-    tensor is held to 4x the fp32 reference's worst error over the parameter set."""
+    """Weight gradients WITHOUT matched ReLU branches (the bench-size render test): a ReLU
+    whose pre-activation lies within fp32 rounding of 0 flips its mask between any two
+    fp32 evaluations, and with random-sign upstream gradients one flipped (point, unit)
+    moves a weight-gradient entry by ~1/sqrt(P) of the tensor's max; which tensor a flip
+    lands in is chance.  So each tensor is held to 4x the fp32 reference's worst error over
+    the parameter set.  The points test below separates the two effects instead."""
     scale = max(rel(ref32[n], truth[n]) for n in truth)
     for n in truth:
         e = rel(got[n], truth[n])
         assert e <= max(4 * scale, floor), f"{n}: HIP {e:.3g} vs fp32 reference worst {scale:.3g}"
 
 
+def _hip_relu_masks(raw, P):
+    """The ReLU branches the HIP forward took: its saved activations h_l = relu(z_l) > 0
+    (nc_imap_points_activation_offset into the forward's workspace, kept by ImapEvalFn)."""
+    import ctypes
+    from nicecore import _lib as L
+    node = raw.grad_fn  # the ImapEvalFn node holds the forward's args and workspace
+    assert hasattr(node, "ws") and hasattr(node, "args")
+    lib = L.load()
+    masks = []
+    for layer in range(4):
+        off = lib.nc_imap_points_activation_offset(ctypes.byref(node.args), layer)
+        assert off >= 0 and off + P * 256 * 4 <= node.ws.numel()
+        h = node.ws[off:off + P * 256 * 4].view(torch.float32).view(P, 256)
+        masks.append((h > 0).cpu())
+    return masks
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("P", [1, 77, 20000])
 def test_imap_points_forward_backward_vs_oracle(P):
     """MLP.forward(p) on caller points (ragged sizes, tile tails) and its backward vs autograd
-    through the oracle (fp32, and float64 as ground truth)."""
+    through the oracle.  Gradients are scored per tensor against a float64 truth evaluated
+    on the HIP forward's own ReLU branches (oracle imap_forward(masks=...)), each within 4x
+    the error of the fp32 oracle on those branches; separately, the HIP branches may
+    differ from the float64 ones in no more (point, unit) pairs than the fp32 oracle's own
+    branches do (x4 + 8): a wrong layer, offset or ldb shows up in one or the other."""
     bound, params = _scene()
     g = torch.Generator().manual_seed(P)
     p = (torch.rand(P, 3, generator=g, dtype=torch.float64) * 1.2 - 0.1)
     m = _model(params)
     pg = p.cuda().requires_grad_(True)
     raw = m(pg)
+    masks = _hip_relu_masks(raw, P)
     up = torch.randn(P, 4, generator=g)
     raw.backward(up.cuda())
 
-    def run(dtype):
+    def run(dtype, mk=None):
         prm = {k: v.to(dtype).clone().requires_grad_(True) for k, v in params.items()}
         pc = p.clone().requires_grad_(True)
-        out = IO.imap_forward(pc, prm)
+        out = IO.imap_forward(pc, prm, mk)
         out.backward(up.to(dtype))
         return out, pc.grad, prm
 
-    ref, ref_gp, ref_prm = run(torch.float32)
-    tru, tru_gp, tru_prm = _f64_truth(run)
+    ref, _, _ = run(torch.float32)
     assert rel(raw, ref) <= OUT_TOL
+    ref_m, ref_gp, ref_prm = run(torch.float32, masks)
+    tru_m, tru_gp, tru_prm = _f64_truth(lambda dt: run(dt, masks))
     _within(pg.grad, ref_gp, tru_gp, "points")
-    _within_set({n: q.grad for n, q in m.named_parameters()}, {n: v.grad for n, v in ref_prm.items()},
-                {n: v.grad for n, v in tru_prm.items()})
+    for n, q in m.named_parameters():
+        _within(q.grad, ref_prm[n].grad, tru_prm[n].grad, n)
+    # branch flips against float64's own branches
+    m32 = IO.imap_relu_masks(p, {k: v.float() for k, v in params.items()})
+    m64 = _f64_truth(lambda dt: IO.imap_relu_masks(p, {k: v.to(dt) for k, v in params.items()}))
+    flips_hip = sum(int((a != b).sum()) for a, b in zip(masks, m64))
+    flips_ref = sum(int((a != b).sum()) for a, b in zip(m32, m64))
+    assert flips_hip <= 4 * flips_ref + 8, (flips_hip, flips_ref)
 
 
 @pytest.mark.gpu
@@ -225,3 +254,20 @@ def test_imap_empty_batch():
     (d.sum() + c.sum()).backward()
     assert d.shape == (0,) and c.shape == (0, 3)
     assert all(float(p.grad.abs().max()) == 0.0 for p in m.parameters())
+
+
+@pytest.mark.gpu
+def test_imap_refuses_deterministic_request(monkeypatch):
+    """The iMAP* weight gradients are split-K float-atomic sums: a deterministic request
+    (NC_DETERMINISTIC=1, as the NICE path honours it) is refused while parameters need
+    gradients, and allowed for a frozen MLP (tracker mode: no weight gradients)."""
+    from nicecore import _lib as L
+    bound, params = _scene()
+    p = torch.rand(64, 3, dtype=torch.float64).cuda()
+    m = _model(params)
+    monkeypatch.setenv("NC_DETERMINISTIC", "1")
+    with pytest.raises(L.NiceCoreError, match="deterministic"):
+        m(p)
+    for q in m.parameters():
+        q.requires_grad_(False)
+    assert m(p).shape == (64, 4)
