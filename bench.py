@@ -338,24 +338,56 @@ def make_step(w, args, world, device):
     return eager, graphed
 
 
-def algorithmic_flops_per_ray(stage, S, mode, fix_fine=False):
-    """Algorithmic FLOP per ray of each decoder kernel:
-    k_mlp_fwd = decoder MACs + trilinear lookups, k_mlp_dx = dX-chain MACs,
-    k_mlp_dw = weight-gradient MACs (BA mode only)."""
-    decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
-            "color": ["fine", "middle", "color"]}[stage]
-    lk_fwd = {"coarse": 1, "middle": 1, "fine": 3, "color": 4}[stage]
-    fwd = 2 * sum(MAC[d] for d in decs) + TRI_FLOP * lk_fwd
-    dx = 2 * sum(MAC_DX[d] for d in decs)
-    dw = 2 * sum(MAC[d] for d in decs if not fix_fine or d == "color") if mode == "ba" else 0
-    return {"k_mlp_fwd": fwd * S, "k_mlp_dx": dx * S, "k_mlp_dw": dw * S,
-            "k_grid_gather": TRI_FLOP * LOOKUPS_UNIQUE[stage] * S}
-
-
+STAGE_DECODERS = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
+                  "color": ["fine", "middle", "color"]}
 # distinct trilinear lookups per point (k_grid_gather reads grid_middle once for the fine
 # and middle decoders, MlpCtx::share_mid); lk_fwd of them are written out
 LOOKUPS_UNIQUE = {"coarse": 1, "middle": 1, "fine": 2, "color": 3}
 LOOKUPS_FWD = {"coarse": 1, "middle": 1, "fine": 3, "color": 4}
+LOOKUP_BYTES = 8 * 32 * 4  # one trilinear lookup: 8 corner rows of 32 f32 channels
+
+
+def algorithmic_per_point(stage, mode, fix_fine=False):
+    """SURVEY.md §8(d)'s fixed convention, per sample point, per kernel: FLOP and HBM bytes.
+
+    FLOP: forward = 2 MAC + trilinear (8 corners x 32 ch x 2 per lookup); dX = 2 MAC of the
+    dX chains (the fine decoder's fc_c input gradient only for its own 32 grid channels:
+    the middle features enter under no_grad, decoder.py:196-202) + trilinear backward (2x
+    the forward trilinear per gradient lookup); dW = 2 MAC (BA mode).
+    Bytes: forward = L_fwd lookups x 1,024 B; backward = per gradient lookup (each decoder
+    samples its own grid with grad) the coordinate-gradient re-gather (1,024 B) plus, in BA
+    mode, the grid-gradient scatter as a read-modify-write of the 8 corner rows (2 x 1,024 B);
+    dW has no §8(d) bytes (its operands are the core's own intermediates).  At stage color,
+    S = 48: 196,608 B/ray forward, 638,976 B/ray in BA mode -- SURVEY.md:461-462."""
+    decs = STAGE_DECODERS[stage]
+    ba = mode == "ba"
+    lk_fwd, lk_grad = LOOKUPS_FWD[stage], len(decs)
+    flop = {"k_mlp_fwd": 2 * sum(MAC[d] for d in decs) + TRI_FLOP * lk_fwd,
+            "k_mlp_dx": 2 * sum(MAC_DX[d] for d in decs) + 2 * TRI_FLOP * lk_grad,
+            "k_mlp_dw": 2 * sum(MAC[d] for d in decs if not fix_fine or d == "color") if ba else 0,
+            "k_grid_gather": TRI_FLOP * LOOKUPS_UNIQUE[stage]}
+    byt = {"k_mlp_fwd": LOOKUP_BYTES * lk_fwd,
+           "k_mlp_dx": LOOKUP_BYTES * lk_grad * (3 if ba else 1),
+           "k_mlp_dw": 0,
+           "k_grid_gather": LOOKUP_BYTES * LOOKUPS_UNIQUE[stage]}
+    return flop, byt
+
+
+def step_roofline_rays_s(stage, S, mode, fix_fine=False):
+    """§8(d) roofline rays/s of one GPU for the whole step (SURVEY.md:461-463): FLOP per ray =
+    forward (2 MAC + trilinear) + dX (2 MAC) [+ dW (2 MAC), BA] + trilinear backward (2x the
+    forward's); bytes per ray = the forward's and backward's lookups above; rays/s =
+    min(f32 peak / FLOP, HBM peak / bytes).  Stage color, S = 48, BA: 15.17 MFLOP and
+    638,976 B per ray -> 10.37 M rays/s."""
+    decs = STAGE_DECODERS[stage]
+    ba = mode == "ba"
+    mac = sum(MAC[d] for d in decs)
+    mac_dw = sum(MAC[d] for d in decs if not fix_fine or d == "color") if ba else 0
+    tri = TRI_FLOP * LOOKUPS_FWD[stage]
+    f_ray = S * (2 * mac + tri + 2 * mac + 2 * mac_dw + 2 * tri)
+    _, byt = algorithmic_per_point(stage, mode, fix_fine)
+    b_ray = S * (byt["k_mlp_fwd"] + byt["k_mlp_dx"])
+    return min(FP32_MFMA_PEAK_TFLOPS * 1e12 / f_ray, HBM_PEAK_GBS * 1e9 / b_ray), f_ray, b_ray
 
 
 # point-record geometry of the core (csrc/nc_mlp.hip Rec<KIND>): floats per point
@@ -365,25 +397,19 @@ FEAT = {"coarse": 32, "middle": 32, "fine": 64, "color": 32}
 NOUT = {"coarse": 1, "middle": 1, "fine": 1, "color": 3}
 
 
-def algorithmic_bytes_per_point(stage, mode, jac=False, fix_fine=False):
-    """HBM bytes a kernel must move per sample point: its inputs and
-    outputs, the saved activation records included (they are the backward's input)."""
-    decs = {"coarse": ["coarse"], "middle": ["middle"], "fine": ["fine", "middle"],
-            "color": ["fine", "middle", "color"]}[stage]
-    fwd = sum(4 * FEAT[d] + 16 + 4 * (REC_LEN[d] - FEAT[d]) + 4 * NOUT[d] for d in decs)
-    # k_mlp_dx per decoder: masks 32 B + d out + p.float() 16 B + normalised xyz 16 B in,
-    # point gradient 24 B out, and for the coordinate gradient either the 8 corner rows
-    # re-gathered (1,024 B, SURVEY.md §8(d)) or the saved trilinear Jacobian (384 B,
-    # NC_SAVE_POINT_JACOBIAN); BA mode adds the backward record out and the grid-gradient
-    # scatter, counted as §8(d) does: 2 x 1,024 B (read-modify-write of 8 corner rows)
+def intermediate_bytes_per_point(stage, mode, jac=False, fix_fine=False):
+    """Bytes per point each kernel moves through the core's OWN intermediates (activation
+    records, point I/O, masks) -- not §8(d) algorithmic traffic, reported beside it
+    (roofline.intermediate_bytes_per_launch).  k_mlp_fwd writes the forward record, k_mlp_dx
+    reads masks / d out / coordinates and writes the backward record, k_mlp_dw streams both."""
+    decs = STAGE_DECODERS[stage]
     ba = mode == "ba"
     wdw = [d for d in decs if not fix_fine or d == "color"] if ba else []  # decoders with dW
-    dx = sum(32 + 4 * NOUT[d] + 16 + 16 + 24 + (384 if jac else 1024) +
-             (2 * 1024 if ba else 0) + (4 * (REC_STRIDE[d] - REC_LEN[d]) if d in wdw else 0) for d in decs)
+    fwd = sum(4 * FEAT[d] + 16 + 4 * (REC_LEN[d] - FEAT[d]) + 4 * NOUT[d] for d in decs)
+    dx = sum(32 + 4 * NOUT[d] + 16 + 16 + 24 - (1024 - 384 if jac else 0) +
+             (4 * (REC_STRIDE[d] - REC_LEN[d]) if d in wdw else 0) for d in decs)
     dw = sum(4 * REC_STRIDE[d] for d in wdw)
-    # k_grid_gather: 8 corner rows of 128 B per distinct lookup, 128 B of features out per
-    # lookup, and the 384-B trilinear Jacobian of each decoder's own lookup (ray gradients)
-    gather = 1024 * LOOKUPS_UNIQUE[stage] + 128 * LOOKUPS_FWD[stage] + (384 * len(decs) if jac else 0)
+    gather = 128 * LOOKUPS_FWD[stage] + (384 * len(decs) if jac else 0)
     return {"k_mlp_fwd": fwd, "k_mlp_dx": dx, "k_mlp_dw": dw, "k_grid_gather": gather}
 
 
@@ -439,8 +465,8 @@ def read_traffic(args):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc
     summary (profiles/*traffic*.json) measured on this same workload, if present."""
     import glob
-    want = {"scene": args.scene, "rays": args.rays, "stage": args.stage, "mode": args.mode,
-            "layout": args.layout}
+    want = traffic_config(args)
+    # newest round first (profiles/r03/... sorts after profiles/r02/...)
     for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*traffic*.json"), recursive=True), reverse=True):
         try:
             with open(fn) as f:
@@ -448,8 +474,15 @@ def read_traffic(args):
         except Exception:
             continue
         if d.get("config") == want:
+            d["source"] = os.path.relpath(fn, REPO)
             return d
     return None
+
+
+def traffic_config(args):
+    """The workload key a PMC traffic summary is valid for (tools/pmc_traffic.py --config)."""
+    return {"scene": args.scene, "rays": args.rays, "stage": args.stage, "mode": args.mode,
+            "layout": args.layout, "fix_fine": bool(args.fix_fine), "render_depth": args.render_depth}
 
 
 class _NullTimer:
@@ -550,32 +583,44 @@ def main():
     avg_ms = ms_dom / max(n_dom, 1)
 
     S = samples_per_ray(args)
-    per_ray = algorithmic_flops_per_ray(args.stage, S, args.mode, args.fix_fine)
     from nicecore import render_fn as RF
-    per_pt_bytes = algorithmic_bytes_per_point(args.stage, args.mode, jac=RF._SAVE_JAC, fix_fine=args.fix_fine)
-    fl = per_ray[dominant] * args.rays if dominant in per_ray else None
-    by = per_pt_bytes[dominant] * args.rays * S if dominant in per_pt_bytes else None
+    flop_pt, byte_pt = algorithmic_per_point(args.stage, args.mode, args.fix_fine)
+    inter_pt = intermediate_bytes_per_point(args.stage, args.mode, jac=RF._SAVE_JAC, fix_fine=args.fix_fine)
+    points = args.rays * S  # units one launch processes
     roof = None
-    if fl is not None and by and avg_ms > 0:
-        tflops = fl / (avg_ms * 1e-3) / 1e12
-        gbs = by / (avg_ms * 1e-3) / 1e9
-        tr = read_traffic(args)
-        traffic = ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes")
+    if dominant in flop_pt and avg_ms > 0:
+        fl = flop_pt[dominant] * points
+        by = byte_pt[dominant] * points
+        t = avg_ms * 1e-3
+        tflops = fl / t / 1e12
+        gbs = by / t / 1e9
         mpeak = MFMA_PEAK.get(dominant, FP32_MFMA_PEAK_TFLOPS)
         ridge = mpeak * 1e12 / (HBM_PEAK_GBS * 1e9)  # FLOP per byte
-        hbm_bound = fl / by < ridge
+        hbm_bound = by > 0 and fl / by < ridge
+        tr = read_traffic(args)
+        traffic = ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes")
         roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dominant,
                 "achieved": round(gbs if hbm_bound else tflops, 3),
                 "peak": HBM_PEAK_GBS if hbm_bound else mpeak,
                 "unit": "GB/s" if hbm_bound else "TFLOP/s",
                 "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / mpeak, 4),
-                "traffic": traffic, "avg_launch_ms": round(avg_ms, 4),
-                "flop_per_launch": fl, "bytes_per_launch": by,
-                "intensity_flop_per_byte": round(fl / by, 2), "ridge_flop_per_byte": round(ridge, 2),
+                "traffic": traffic,
+                "traffic_source": (tr or {}).get("source"),
+                "traffic_frac": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                "avg_launch_ms": round(avg_ms, 4),
+                "points_per_launch": points,
+                "bytes_per_point": byte_pt[dominant], "flop_per_point": flop_pt[dominant],
+                "bytes_per_launch": by, "flop_per_launch": fl,
+                "bytes_convention": "SURVEY.md §8(d): 1,024 B per trilinear lookup read; grid-gradient "
+                                    "scatter = read-modify-write of the 8 corner rows (2 x 1,024 B)",
+                "intermediate_bytes_per_launch": inter_pt.get(dominant, 0) * points,
+                "intensity_flop_per_byte": round(fl / by, 2) if by else None,
+                "ridge_flop_per_byte": round(ridge, 2),
                 "mfma_tflops": round(tflops, 3), "mfma_peak_tflops": round(mpeak, 1),
                 "mfma_frac": round(tflops / mpeak, 4),
                 "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                 "timing": timing_src}
+    peak_rays, f_ray, b_ray = step_roofline_rays_s(args.stage, S, args.mode, args.fix_fine)
 
     value = world * args.rays * args.steps / dt
     out = {
@@ -600,6 +645,9 @@ def main():
                    "overlap": "grid all-reduce beside k_mlp_dw" if (w["ba"] and w["sparse"] is None and (
                        args.overlap == "on" or (args.overlap == "auto" and world > 1))) else "none"},
         "roofline": roof,
+        "step_roofline": {"rays_s_per_gpu_peak": round(peak_rays), "flop_per_ray": f_ray, "bytes_per_ray": b_ray,
+                          "frac": round(value / world / peak_rays, 4),
+                          "note": "SURVEY.md §8(d): min(157.3 TF / FLOP per ray, 8 TB/s / bytes per ray)"},
         "launch": "hipGraph replay" if graphed is not None else "eager",
         "eager_ms_per_step": round(eager_ms, 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1])},

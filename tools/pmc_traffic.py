@@ -4,7 +4,11 @@ MI355X_MICROARCH.md § HBM: FETCH_SIZE counts half the bytes of wide coalesced
 reads (x2); WRITE_SIZE is exact for 16-B stores and float atomics.
 FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB.
 
-    python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json]
+    python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [bench args...]]
+
+With bench args (the same ones the profiled bench.py run had), the summary gets the
+"config" key bench.py's read_traffic() matches (bench.traffic_config), so a bench line
+only ever quotes traffic measured on its own workload.
 """
 import csv
 import json
@@ -12,9 +16,21 @@ import sys
 from collections import defaultdict
 
 
+def _csv(path):
+    """A counter_collection.csv, or the rocprofv3 output directory holding one."""
+    import glob
+    import os
+    if os.path.isdir(path):
+        hits = sorted(glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True))
+        if not hits:
+            raise SystemExit(f"no counter_collection.csv under {path}")
+        return hits[0]
+    return path
+
+
 def per_kernel(path, counter):
     acc = defaultdict(list)
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(open(_csv(path))):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
@@ -41,6 +57,13 @@ if __name__ == "__main__":
                   "launches": [nf, nw]}
         print(f"{k:22s} read {rd / 1e6:9.2f} MB  write {wr / 1e6:9.2f} MB  ({nf}/{nw} launches)")
     if len(sys.argv) > 3:
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        bargs = sys.argv[4:]
+        saved, sys.argv = sys.argv, ["bench.py", *bargs]
+        cfg = bench.traffic_config(bench.parse())
+        sys.argv = saved
         json.dump({"note": "HBM bytes per launch, rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) "
                            "and WRITE_SIZE in separate passes; see tools/pmc_traffic.py",
-                   "kernels": out}, open(sys.argv[3], "w"), indent=1)
+                   "config": cfg, "bench_args": bargs, "kernels": out}, open(sys.argv[3], "w"), indent=1)

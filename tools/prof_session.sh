@@ -22,4 +22,5 @@ run stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stat
 run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- \
     python3 "$ROOT/bench.py" "$@" --cpu-seconds 0 &&
 run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- \
-    python3 "$ROOT/bench.py" "$@" --cpu-seconds 0
+    python3 "$ROOT/bench.py" "$@" --cpu-seconds 0 &&
+python3 "$ROOT/tools/pmc_traffic.py" "$out/fetch" "$out/write" "$out/hbm_traffic.json" "$@"
