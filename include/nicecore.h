@@ -294,6 +294,36 @@ typedef struct nc_frustum_args {
 
 int nc_frustum_mask(const nc_frustum_args* args, void* stream);
 
+/* Frustum feature selection's masked grid rows (ABI v8, additive): the Mapper keeps the
+ * voxels inside the frame's frustum as one optimisable tensor and writes it into the grid
+ * every iteration and back after the optimiser step (src/Mapper.py:393-404 val[mask]
+ * .clone(), :491-500 val[mask] = val_grad, :633-642 the write-back; the backward of
+ * that index_put is grad[mask]).  Here the mask is the list of its voxels, rows[n]
+ * (ascending voxel index z*H*W + y*W + x, as mask.nonzero() gives them, computed once per
+ * frame), and the optimisable tensor is laid out as ATen's val[mask] for the mask
+ * repeated over the C channels: packed[c * n + i] = grid[0, c, voxel rows[i]].
+ *   NC_ROWS_GATHER   packed <- grid rows   (val[mask], grad[mask])
+ *   NC_ROWS_SCATTER  grid rows <- packed   (val[mask] = val_grad)
+ *   NC_ROWS_ZERO     grid rows <- 0        (the index_put backward's gradient of val)
+ * grid: [1, C, D, H, W] float32 with any strides (channels-last: one 128-B row per
+ * voxel, transposed through LDS).  Plain copies: bit-identical to ATen's. */
+#define NC_ROWS_GATHER 0
+#define NC_ROWS_SCATTER 1
+#define NC_ROWS_ZERO 2
+typedef struct nc_grid_rows_args {
+  int32_t abi_version;
+  int32_t op;                  /* NC_ROWS_* */
+  int64_t n_rows;
+  const int64_t* rows;         /* [n_rows] voxel indices, each < D*H*W */
+  float* grid;                 /* element (c, z, y, x) at c*stride[0] + z*stride[1] + y*stride[2] + x*stride[3] */
+  int64_t channels;            /* C */
+  int64_t dims[3];             /* D, H, W */
+  int64_t stride[4];           /* elements */
+  float* packed;               /* [C][n_rows] */
+} nc_grid_rows_args;
+
+int nc_grid_rows(const nc_grid_rows_args* args, void* stream);
+
 /* Hierarchical (importance) sampling, sample_pdf (src/common.py:19-63), as
  * render_batch_ray applies it when N_importance > 0 (src/utils/Renderer.py:244-250):
  * per ray, N inverse-CDF samples of the piecewise-constant pdf weights + 1e-5 over
@@ -407,7 +437,8 @@ int64_t nc_param_count(int decoder);
 
 /* sizeof() of the ABI structs, for binding-layout checks:
  * 0 nc_render_args, 1 nc_points_args, 2 nc_grid, 3 nc_decoder_params, 4 nc_sample_args, 5 nc_frustum_args,
- * 6 nc_sparse_rows, 7 nc_pdf_args, 8 nc_adam_args, 9 nc_adam_segment. */
+ * 6 nc_sparse_rows, 7 nc_pdf_args, 8 nc_adam_args, 9 nc_adam_segment, 10 nc_imap_render_args,
+ * 11 nc_imap_points_args, 12 nc_imap_params, 13 nc_grid_rows_args. */
 size_t nc_struct_size(int which);
 
 size_t nc_render_workspace_bytes(const nc_render_args* args);

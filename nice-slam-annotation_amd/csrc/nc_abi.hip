@@ -37,14 +37,15 @@ enum KernelId {
   KID_DEPTH_MAX = 0, KID_RAY_SETUP, KID_MLP_FWD, KID_COMPOSITE_FWD, KID_COMPOSITE_BWD, KID_MLP_DX,
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
   KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
-  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_ADAM, KID_IMAP_GEMM, KID_IMAP_FOURIER, KID_COUNT
+  KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_ADAM, KID_IMAP_GEMM, KID_IMAP_FOURIER, KID_GRID_ROWS,
+  KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
                                        "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce", "k_sample_pdf", "k_adam",
-                                       "k_imap_gemm", "k_imap_fourier"};
+                                       "k_imap_gemm", "k_imap_fourier", "k_grid_rows"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -643,6 +644,7 @@ size_t nc_struct_size(int which) {
     case 10: return sizeof(nc_imap_render_args);
     case 11: return sizeof(nc_imap_points_args);
     case 12: return sizeof(nc_imap_params);
+    case 13: return sizeof(nc_grid_rows_args);
   }
   return 0;
 }
@@ -849,6 +851,20 @@ int nc_sample_rays_backward(const nc_sample_args* a, void* stream) {
   if (!a->g_c2w) return fail(-1, "nicecore: NULL pose gradient output");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return check_hip(timed(KID_SAMPLE_POSE_GRAD, s, [&] { return launch_sample_pose_grad(*a, s); }), "k_sample_pose_grad");
+}
+
+int nc_grid_rows(const nc_grid_rows_args* a, void* stream) {
+  if (!a) return fail(-1, "nicecore: args is NULL");
+  if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
+  if (a->op != NC_ROWS_GATHER && a->op != NC_ROWS_SCATTER && a->op != NC_ROWS_ZERO)
+    return fail(-1, "nicecore: nc_grid_rows: unknown op");
+  if (a->n_rows < 0 || a->channels <= 0 || a->dims[0] <= 0 || a->dims[1] <= 0 || a->dims[2] <= 0)
+    return fail(-1, "nicecore: nc_grid_rows: bad sizes");
+  if (a->n_rows > 0 && (!a->rows || !a->grid || (a->op != NC_ROWS_ZERO && !a->packed)))
+    return fail(-1, "nicecore: nc_grid_rows: NULL pointer");
+  if (a->n_rows * a->channels >= (int64_t(1) << 40)) return fail(-1, "nicecore: nc_grid_rows: too many rows");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return check_hip(timed(KID_GRID_ROWS, s, [&] { return launch_grid_rows(*a, s); }), "k_grid_rows");
 }
 
 int nc_frustum_mask(const nc_frustum_args* a, void* stream) {

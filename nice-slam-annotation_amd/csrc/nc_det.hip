@@ -5,16 +5,15 @@
 // NC_DETERMINISTIC, k_mlp_dx stores each point's feature gradient instead
 // (MlpCtx::dfeat) and this file reduces them in a fixed order:
 //   k_det_keys    entry (job, point, corner) -> key (job << vbits | voxel), weight
-//   radix sort    rocprim's stable LSD radix sort of (key, entry id): the entries of
-//                 one voxel end up adjacent, in ascending (point, corner) order
+//   radix sort    a stable LSD radix sort of (key, entry id), 8 bits per pass, written
+//                 here (k_rs_hist -> k_rs_scan -> k_rs_scatter): the entries of one voxel
+//                 end up adjacent, in ascending (point, corner) order
 //   k_det_runs /  each voxel run is summed (w * d feature, channel per lane) in
 //   k_det_join    entry order, 32 entries per half-wave, boundary pieces joined in
 //                 order; one writer per voxel (no atomics)
 // The order is the reference's own: ATen's CPU grid_sampler_3d_backward walks points
 // in order and adds each point's 8 corner contributions (gInp += gOut * w), and a
 // voxel is a corner of a point at most once.
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include "nc_device.h"
 #include "nc_internal.h"
 
@@ -120,12 +119,12 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   const int64_t s = (int64_t)blockIdx.x * 8 + hw;
   const int64_t e0 = s * DSUB;
   const int cnt = e0 >= n ? 0 : (int)(n - e0 < DSUB ? n - e0 : DSUB);
-  const K* key = reinterpret_cast<const K*>(d.key[1]);
+  const K* key = reinterpret_cast<const K*>(d.key[d.sorted]);
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   // the sub-chunk's entries, one per lane (coalesced), then every entry's weighted
   // feature-gradient row in flight at once
   const K myk = ch < cnt ? key[e0 + ch] : invalid;
-  const uint32_t ent = ch < cnt ? d.val[1][e0 + ch] : 0u;
+  const uint32_t ent = ch < cnt ? d.val[d.sorted][e0 + ch] : 0u;
   const float myw = ch < cnt ? d.w[ent] : 0.f;
   float v[DSUB];
 #pragma unroll
@@ -180,7 +179,7 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
   const int64_t e0 = s * DSUB;
   if (e0 >= n) return;
   const int64_t e1 = e0 + DSUB < n ? e0 + DSUB : n;
-  const K* key = reinterpret_cast<const K*>(d.key[1]);
+  const K* key = reinterpret_cast<const K*>(d.key[d.sorted]);
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   const K last = key[e1 - 1];
   if (last == invalid || e1 >= n || key[e1] != last) return;  // no run continues past s
@@ -195,35 +194,183 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
   det_add(m, d, last, ch, acc);
 }
 
-// rocprim's merge-sort path at every size: its onesweep path (taken above 1M items by
-// default) spins on decoupled look-back flags, and inside a replayed hipGraph it hung
-// or returned garbage order here (NC_DETERMINISTIC at C2, 1.15M entries); the merge
-// path is plain block-sort and merge kernels
-using DetSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                 rocprim::default_config, (size_t(1) << 40)>;
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort of (key, entry id), RS_BITS per pass, for the deterministic
+// scatter.  Reduce-then-scan: every pass is three plain kernels whose state is entirely
+// rewritten by the pass itself -- no memsets, no counters carried between launches, no
+// workgroup waiting on another (a hipGraph replays it like any other kernel chain).
+// This replaces rocprim's radix sort here: its onesweep path (taken above 1M items)
+// resets a decoupled look-back state and an atomic block-id counter with two
+// hipMemsetAsync per digit pass and then spins on other workgroups' flags; in the
+// captured graph those resets are memset nodes, and a look-back state not yet zeroed
+// when the pass starts reads as a predecessor's COMPLETE prefix of the previous pass or
+// replay (scatter offsets off -> entry ids never written -> the faulting gather that was
+// seen) or a stale block id whose predecessor never publishes (the look-back spin that
+// was seen).  Both recorded failures are that one mechanism; the sort below has none of
+// it: it is capture-safe by construction, and faster at these sizes.
+//   k_rs_hist     tile of RS_TILE keys per workgroup -> its digit counts, digit-major
+//                 hist[d][tile]
+//   k_rs_scan     one workgroup per digit: exclusive scan of hist[d][*] in place, total[d]
+//   k_rs_scatter  tile rank by rank: 256 entries per round in input order, stable rank
+//                 inside the wave from 8 ballots, wave offsets through LDS; destination =
+//                 exclusive scan of total[] + hist[d][tile] + rank so far
+// ---------------------------------------------------------------------------
+constexpr int RS_BITS = 8;
+constexpr int RS_BINS = 1 << RS_BITS;
+constexpr int RS_THREADS = 256;
+constexpr int RS_ROUNDS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;
 
 template <typename K>
-static size_t sort_temp_bytes(int64_t n_entries, int end_bit) {
-  size_t bytes = 0;
-  if (rocprim::radix_sort_pairs<DetSortConfig>(nullptr, bytes, (K*)nullptr, (K*)nullptr, (uint32_t*)nullptr,
-                                               (uint32_t*)nullptr, (size_t)n_entries, 0, (unsigned)end_bit) != hipSuccess)
-    return 0;
-  return bytes ? bytes : 1;
+__device__ __forceinline__ int rs_digit(K k, int bit) {
+  return (int)((k >> bit) & (K)(RS_BINS - 1));
 }
+
+template <typename K>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* __restrict__ key, int64_t n, int bit,
+                                                        uint32_t* __restrict__ hist, int64_t ntile) {
+  __shared__ uint32_t cnt[RS_BINS];
+  cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int64_t e = base + r * RS_THREADS + threadIdx.x;
+    if (e < n) atomicAdd(&cnt[rs_digit(key[e], bit)], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * ntile + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// block-wide exclusive scan of one value per thread (RS_THREADS = 4 waves); returns the
+// block total through *total
+__device__ __forceinline__ uint32_t rs_block_exscan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int q = 0; q < RS_THREADS / 64; ++q) {
+    before += q < w ? wsum[q] : 0u;
+    all += wsum[q];
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_scan(uint32_t* __restrict__ hist, int64_t ntile,
+                                                        uint32_t* __restrict__ total) {
+  __shared__ uint32_t wsum[RS_THREADS / 64];
+  uint32_t* row = hist + (int64_t)blockIdx.x * ntile;
+  const int64_t per = (ntile + RS_THREADS - 1) / RS_THREADS;
+  const int64_t a = threadIdx.x * per, b = a + per < ntile ? a + per : ntile;
+  uint32_t s = 0;
+  for (int64_t i = a; i < b; ++i) s += row[i];
+  uint32_t all;
+  uint32_t run = rs_block_exscan(s, wsum, &all);
+  for (int64_t i = a; i < b; ++i) {
+    const uint32_t c = row[i];
+    row[i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) total[blockIdx.x] = all;
+}
+
+template <typename K>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                           K* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n,
+                                                           int bit, const uint32_t* __restrict__ hist, int64_t ntile,
+                                                           const uint32_t* __restrict__ total) {
+  __shared__ uint32_t start[RS_BINS];                 // next output slot of each digit for this tile
+  __shared__ uint32_t wcnt[RS_THREADS / 64][RS_BINS];  // this round's count of each digit per wave
+  __shared__ uint32_t wsum[RS_THREADS / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  {
+    uint32_t all;
+    const uint32_t base = rs_block_exscan(total[threadIdx.x], wsum, &all);
+    start[threadIdx.x] = base + hist[(int64_t)threadIdx.x * ntile + blockIdx.x];
+  }
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int64_t tile0 = (int64_t)blockIdx.x * RS_TILE;
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int64_t e = tile0 + r * RS_THREADS + threadIdx.x;
+    if (tile0 + r * RS_THREADS >= n) break;  // block-uniform
+#pragma unroll
+    for (int q = 0; q < RS_THREADS / 64; ++q) wcnt[q][threadIdx.x] = 0u;
+    const bool ok = e < n;
+    const K k = ok ? kin[e] : (K)0;
+    const uint32_t v = ok ? vin[e] : 0u;
+    const int d = rs_digit(k, bit);
+    // lanes of this wave holding the same digit (and a valid entry)
+    uint64_t same = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < RS_BITS; ++b) {
+      const uint64_t m = __ballot((d >> b) & 1);
+      same &= ((d >> b) & 1) ? m : ~m;
+    }
+    const uint32_t rank = (uint32_t)__popcll(same & below);
+    __syncthreads();  // wcnt zeroed; start[] of the previous round updated
+    if (ok && rank == 0) wcnt[w][d] = (uint32_t)__popcll(same);
+    __syncthreads();
+    if (ok) {
+      uint32_t off = start[d] + rank;
+#pragma unroll
+      for (int q = 0; q < RS_THREADS / 64; ++q) off += q < w ? wcnt[q][d] : 0u;
+      kout[off] = k;
+      vout[off] = v;
+    }
+    __syncthreads();
+    {
+      uint32_t add = 0;
+#pragma unroll
+      for (int q = 0; q < RS_THREADS / 64; ++q) add += wcnt[q][threadIdx.x];
+      start[threadIdx.x] += add;
+    }
+  }
+}
+
+static int64_t rs_tiles(int64_t n) { return (n + RS_TILE - 1) / RS_TILE; }
 
 size_t det_sort_temp_bytes(int64_t n_entries, int end_bit) {
-  return end_bit <= 32 ? sort_temp_bytes<uint32_t>(n_entries, end_bit) : sort_temp_bytes<uint64_t>(n_entries, end_bit);
+  (void)end_bit;
+  return (size_t)(RS_BINS * rs_tiles(n_entries) + RS_BINS) * 4;
+}
+
+// sorts (key[0], val[0]) by the low end_bit bits; returns the buffer index holding the result
+template <typename K>
+static int radix_sort(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, int* sorted) {
+  const int64_t nt = rs_tiles(n);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(d.temp);
+  uint32_t* total = hist + RS_BINS * nt;
+  int src = 0;
+  for (int bit = 0; bit < end_bit; bit += RS_BITS) {
+    const K* kin = reinterpret_cast<const K*>(d.key[src]);
+    K* kout = reinterpret_cast<K*>(d.key[1 - src]);
+    hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, n, bit, hist, nt);
+    hipLaunchKernelGGL(k_rs_scan, dim3(RS_BINS), dim3(RS_THREADS), 0, s, hist, nt, total);
+    hipLaunchKernelGGL(k_rs_scatter<K>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, d.val[src], kout,
+                       d.val[1 - src], n, bit, hist, nt, total);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+    src = 1 - src;
+  }
+  *sorted = src;
+  return 0;
 }
 
 template <typename K>
-static int det_scatter(const MlpCtx& m, const DetBufs& d, int64_t n, hipStream_t s) {
+static int det_scatter(const MlpCtx& m, const DetBufs& d0, int64_t n, hipStream_t s) {
+  DetBufs d = d0;
   hipLaunchKernelGGL(k_det_keys<K>, dim3((unsigned)((m.P + 255) / 256), m.n_jobs), dim3(256), 0, s, m, d);
   if (hipError_t e = hipGetLastError()) return (int)e;
-  size_t bytes = d.temp_bytes;
-  if (hipError_t e = rocprim::radix_sort_pairs<DetSortConfig>(
-          d.temp, bytes, reinterpret_cast<K*>(d.key[0]), reinterpret_cast<K*>(d.key[1]), d.val[0], d.val[1],
-          (size_t)n, 0, (unsigned)(d.vbits + 2), s))
-    return (int)e;
+  if (d.temp_bytes < det_sort_temp_bytes(n, d.vbits + 2)) return (int)hipErrorInvalidValue;
+  if (int e = radix_sort<K>(d, n, d.vbits + 2, s, &d.sorted)) return e;
   const int64_t nsub = (n + DSUB - 1) / DSUB;
   hipLaunchKernelGGL(k_det_runs<K>, dim3((unsigned)((nsub + 7) / 8)), dim3(256), 0, s, m, d, n);
   if (hipError_t e = hipGetLastError()) return (int)e;

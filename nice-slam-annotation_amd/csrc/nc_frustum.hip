@@ -107,4 +107,82 @@ int launch_frustum_mask(const nc_frustum_args& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Masked grid rows (nc_grid_rows): the Mapper's val[mask] / val[mask] = val_grad /
+// grad[mask] (Mapper.py:393-404, :491-500, :633-642) as copies between the grid's voxel
+// rows and the packed [C][n] tensor.  Channels-last grids (channel stride 1, C = 32): a
+// workgroup moves 64 rows; a row is 8 float4 loads (one 128-B line), the [C][64] side is
+// 64-float runs per channel; the transpose goes through LDS (row pitch 33: conflict-free).
+// Other strides: one thread per (channel, row), plain strided copies.
+// ---------------------------------------------------------------------------
+constexpr int GR_ROWS = 64;
+
+__global__ void __launch_bounds__(256) k_grid_rows_cl(const nc_grid_rows_args a) {
+  __shared__ float tile[GR_ROWS][33];
+  const int64_t r0 = (int64_t)blockIdx.x * GR_ROWS;
+  const int t = threadIdx.x;
+  const int64_t n = a.n_rows;
+  if (a.op == NC_ROWS_GATHER) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // 64 rows x 8 float4
+      const int q = t + 256 * k, r = q >> 3, c4 = (q & 7) * 4;
+      if (r0 + r < n) {
+        const int64_t v = a.rows[r0 + r];
+        const float4 x = *reinterpret_cast<const float4*>(a.grid + v * a.stride[3] + c4);
+        tile[r][c4] = x.x; tile[r][c4 + 1] = x.y; tile[r][c4 + 2] = x.z; tile[r][c4 + 3] = x.w;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // 32 channels x 64 rows, lane = row
+      const int c = (t >> 6) + 4 * k, r = t & 63;
+      if (r0 + r < n) a.packed[(int64_t)c * n + r0 + r] = tile[r][c];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = (t >> 6) + 4 * k, r = t & 63;
+      if (r0 + r < n) tile[r][c] = a.op == NC_ROWS_ZERO ? 0.f : a.packed[(int64_t)c * n + r0 + r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = t + 256 * k, r = q >> 3, c4 = (q & 7) * 4;
+      if (r0 + r < n) {
+        const int64_t v = a.rows[r0 + r];
+        *reinterpret_cast<float4*>(a.grid + v * a.stride[3] + c4) =
+            float4{tile[r][c4], tile[r][c4 + 1], tile[r][c4 + 2], tile[r][c4 + 3]};
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_grid_rows_any(const nc_grid_rows_args a) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (c, i), i fastest
+  const int64_t n = a.n_rows;
+  if (e >= n * a.channels) return;
+  const int64_t c = e / n, i = e - c * n;
+  const int64_t v = a.rows[i];
+  const int64_t H = a.dims[1], W = a.dims[2];
+  const int64_t x = v % W, y = (v / W) % H, z = v / (W * H);
+  float* g = a.grid + c * a.stride[0] + z * a.stride[1] + y * a.stride[2] + x * a.stride[3];
+  if (a.op == NC_ROWS_GATHER) a.packed[e] = *g;
+  else *g = a.op == NC_ROWS_ZERO ? 0.f : a.packed[e];
+}
+
+static bool grid_rows_cl(const nc_grid_rows_args& a) {
+  const int64_t H = a.dims[1], W = a.dims[2];
+  return a.channels == 32 && a.stride[0] == 1 && a.stride[3] == 32 && a.stride[2] == 32 * W &&
+         a.stride[1] == 32 * W * H && (reinterpret_cast<uintptr_t>(a.grid) & 15u) == 0;
+}
+
+int launch_grid_rows(const nc_grid_rows_args& a, hipStream_t s) {
+  if (a.n_rows == 0) return 0;
+  if (grid_rows_cl(a))
+    hipLaunchKernelGGL(k_grid_rows_cl, dim3((unsigned)((a.n_rows + GR_ROWS - 1) / GR_ROWS)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_grid_rows_any, dim3((unsigned)((a.n_rows * a.channels + 255) / 256)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
 }  // namespace nc

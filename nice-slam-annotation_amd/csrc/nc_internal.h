@@ -85,9 +85,10 @@ struct DetBufs {
   float* w;                  // [n_jobs * P * 8] trilinear weight of each entry
   float* part;               // [ceil(entries / 32)][2][32] partial sums of the runs that cross a
                              // 32-entry sub-chunk boundary (k_det_runs -> k_det_join)
-  void* temp;                // rocprim radix-sort scratch
+  void* temp;                // radix-sort scratch: digit counts per tile + digit totals
   size_t temp_bytes;
   int32_t vbits;             // bits of the voxel index; key = job << vbits | voxel
+  int32_t sorted;            // which of key[] / val[] holds the sorted entries (set by the sort)
 };
 size_t det_sort_temp_bytes(int64_t n_entries, int end_bit);
 int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s);
@@ -97,6 +98,7 @@ int launch_sample_rays(const nc_sample_args& a, hipStream_t s);
 int launch_sample_pose_grad(const nc_sample_args& a, hipStream_t s);
 // frustum feature selection (nc_frustum.hip)
 int launch_frustum_mask(const nc_frustum_args& a, hipStream_t s);
+int launch_grid_rows(const nc_grid_rows_args& a, hipStream_t s);
 // importance sampling (nc_pdf.hip)
 int launch_sample_pdf(const nc_pdf_args& a, hipStream_t s);
 // optimiser step (nc_adam.hip)

@@ -1424,6 +1424,8 @@ int fwd_tile_cost(int kind) {
 #endif
 }
 
+constexpr int EXACT_WGS_PER_JOB = 16;
+
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
   static int attr = -1;
   if (attr != 0 && (attr = set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes()) |
@@ -1440,10 +1442,17 @@ int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_mlp_fwd<false>, grid, dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
   if (hipError_t e = hipGetLastError()) return (int)e;
   if (FWD_F32 || c.range_flag == nullptr) return 0;
+  // the recompute pass runs on a few workgroups per job: its normal cost is the dispatch
+  // of workgroups that read one flag and return (4.7 us for the forward's 256 x 512
+  // threads at C2, rocprofv3), and a flagged job -- never seen with sane inputs -- takes a
+  // few times the forward's time instead of one
+  MlpCtx x = c;
+  for (int j = 0; j <= MAX_JOBS; ++j) x.fwd_off[j] = (j < c.n_jobs ? j : c.n_jobs) * EXACT_WGS_PER_JOB;
+  const dim3 xgrid(x.fwd_off[c.n_jobs]);
   if (c.fuse_gather)
-    hipLaunchKernelGGL(k_mlp_fwd_exact<true>, grid, dim3(FWD_THREADS_FUSED), mlp_fwd_exact_lds_bytes(), s, c);
+    hipLaunchKernelGGL(k_mlp_fwd_exact<true>, xgrid, dim3(FWD_THREADS_FUSED), mlp_fwd_exact_lds_bytes(), s, x);
   else
-    hipLaunchKernelGGL(k_mlp_fwd_exact<false>, grid, dim3(FWD_THREADS), mlp_fwd_exact_lds_bytes(), s, c);
+    hipLaunchKernelGGL(k_mlp_fwd_exact<false>, xgrid, dim3(FWD_THREADS), mlp_fwd_exact_lds_bytes(), s, x);
   return (int)hipGetLastError();
 }
 

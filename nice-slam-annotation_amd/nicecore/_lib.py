@@ -100,6 +100,15 @@ class NcFrustumArgs(ctypes.Structure):
                 ("mask", c_void_p), ("scratch", c_void_p)]
 
 
+class NcGridRowsArgs(ctypes.Structure):
+    _fields_ = [("abi_version", c_int32), ("op", c_int32), ("n_rows", c_int64), ("rows", c_void_p),
+                ("grid", c_void_p), ("channels", c_int64), ("dims", c_int64 * 3), ("stride", c_int64 * 4),
+                ("packed", c_void_p)]
+
+
+NC_ROWS_GATHER, NC_ROWS_SCATTER, NC_ROWS_ZERO = 0, 1, 2
+
+
 class NcSparseRows(ctypes.Structure):
     _fields_ = [("grad_rows", c_void_p), ("n_voxels", c_int64), ("row_voxel", c_void_p),
                 ("row_count", c_void_p), ("capacity", c_int64), ("values", c_void_p)]
@@ -168,6 +177,7 @@ EXPORTS = {
     "nc_sample_rays_forward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
     "nc_sample_rays_backward": (c_int, [POINTER(NcSampleArgs), c_void_p]),
     "nc_frustum_mask": (c_int, [POINTER(NcFrustumArgs), c_void_p]),
+    "nc_grid_rows": (c_int, [POINTER(NcGridRowsArgs), c_void_p]),
     "nc_sample_pdf": (c_int, [POINTER(NcPdfArgs), c_void_p]),
     "nc_adam_step": (c_int, [POINTER(NcAdamArgs), c_void_p]),
     "nc_adam_step_multi": (c_int, [POINTER(NcAdamArgs), POINTER(NcAdamSegment), c_int32, c_void_p]),

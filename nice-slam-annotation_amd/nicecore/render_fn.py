@@ -27,6 +27,9 @@ def _ptr(t):
     return t.data_ptr() if t is not None else None
 
 
+_unflatten = torch._C._nn.unflatten_dense_tensors  # flat, tensors -> views shaped like tensors
+
+
 def _bound_rows(b) -> list:
     """[[lo, hi]] * 3 as Python floats.  For a device-resident bound the rows are
     cached ON the tensor object, tagged with its storage pointer and version counter,
@@ -363,6 +366,8 @@ def _zero_grads(grid_grads, flats):
 
 
 def _split_param_grads(plan, flats, needs_params):
+    """Per-parameter views of each decoder's flat gradient (one C++ call per decoder:
+    unflatten_dense_tensors, instead of a slice + view per parameter in Python)."""
     out = []
     sl = plan.param_slices()
     for k in plan.decs:
@@ -371,11 +376,8 @@ def _split_param_grads(plan, flats, needs_params):
         if k not in flats:
             out += [None] * len(ps)
             continue
-        o = 0
-        for j, p in enumerate(ps):
-            n = p.numel()
-            out.append(flats[k][o:o + n].view_as(p) if needs_params[a + j] else None)
-            o += n
+        views = _unflatten(flats[k], ps)
+        out += [v if needs_params[a + j] else None for j, v in enumerate(views)]
     return out
 
 

@@ -46,7 +46,24 @@ def test_struct_layouts_match(lib):
     assert lib.nc_struct_size(10) == ctypes.sizeof(L.NcImapRenderArgs)
     assert lib.nc_struct_size(11) == ctypes.sizeof(L.NcImapPointsArgs)
     assert lib.nc_struct_size(12) == ctypes.sizeof(L.NcImapParams)
+    assert lib.nc_struct_size(13) == ctypes.sizeof(L.NcGridRowsArgs)
     assert lib.nc_abi_version() == L.NC_ABI_VERSION
+
+
+def test_grid_rows_argument_errors(lib):
+    """nc_grid_rows validates before touching the device (no GPU here)."""
+    a = L.NcGridRowsArgs()
+    a.abi_version = L.NC_ABI_VERSION
+    a.op, a.n_rows, a.channels = 7, 0, 32
+    a.dims[0] = a.dims[1] = a.dims[2] = 4
+    assert lib.nc_grid_rows(ctypes.byref(a), None) == -1  # unknown op
+    a.op = L.NC_ROWS_GATHER
+    a.n_rows = 5  # NULL rows / grid / packed
+    assert lib.nc_grid_rows(ctypes.byref(a), None) == -1
+    a.abi_version = 7
+    assert lib.nc_grid_rows(ctypes.byref(a), None) == -2
+    a.abi_version, a.n_rows = L.NC_ABI_VERSION, 0
+    assert lib.nc_grid_rows(ctypes.byref(a), None) == 0  # nothing to move
 
 
 def test_param_counts_match_modules(lib):

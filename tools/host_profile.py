@@ -16,8 +16,10 @@ if __name__ == "__main__":
     args = bench.parse()
     world, rank, local = bench.setup_dist(args)
     device = torch.device("cuda", 0)
-    w = bench.build_workload(args, rank, device)
-    step = bench.make_step(w, args, world, device)
+    from nicecore import _lib as L
+    L.load()
+    w = bench.build_workload(args, rank, device, world)
+    step, _ = bench.make_step(w, args, world, device)  # the eager step (the drop-in path)
     for _ in range(10):
         step()
     torch.cuda.synchronize()
@@ -37,3 +39,10 @@ if __name__ == "__main__":
     torch.cuda.synchronize()
     pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
     pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    # torch.profiler view of the same step: host time per aten op / autograd node
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU]) as prof:
+        for _ in range(20):
+            step()
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=40))
