@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 8
+#define NC_ABI_VERSION 9
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -149,7 +149,7 @@ typedef struct nc_render_args {
   int32_t n_strat;       /* N_samples (configs/nice_slam.yaml:122) */
   int32_t n_surf;        /* N_surface; must be 0 when gt_depth == NULL or stage == COARSE */
   int32_t flags;         /* NC_SAVE_FOR_BACKWARD (autograd: the graph requires grad) */
-  int32_t reserved;      /* 0 */
+  int32_t lindisp;       /* ABI v9: 1 = stratified depths linear in disparity (Renderer.py:208-209) */
   const float* rays_o;   /* [N,3] */
   const float* rays_d;   /* [N,3] */
   const float* gt_depth; /* [N] or NULL */
@@ -199,6 +199,11 @@ typedef struct nc_render_args {
   int32_t reserved3;
   double* z_out;
   float* weights_out;
+  /* ABI v9: perturb > 0 (Renderer.py:211-219): the stratified depths are jittered inside
+   * their intervals, z = lower + (upper - lower) * t_rand (float64 arithmetic), with the
+   * caller's uniform draws t_rand [N][n_strat] float32 (the reference's
+   * torch.rand(z_vals.shape)); NULL = no perturbation. */
+  const float* t_rand;
 } nc_render_args;
 
 typedef struct nc_points_args {

@@ -470,6 +470,8 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
 void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, const Ws& w, int64_t P, int S) {
   std::memset(&c, 0, sizeof(c));
   c.range_flag = at<uint32_t>(ws, w.rflag);
+  c.lindisp = a->lindisp;
+  c.t_rand = a->t_rand;
   c.N = a->n_rays;
   c.P = P;
   c.S = S;

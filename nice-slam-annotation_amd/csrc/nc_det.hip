@@ -86,27 +86,24 @@ __device__ __forceinline__ uint64_t shfl_key(uint64_t v, int src) {
 // add (not a store) keeps the accumulate contract of nicecore.h: sparse rows collect
 // several forward/backward calls until nc_sparse_rows_clear, and a caller's dense
 // gradient buffer keeps what was in it, exactly as the float-atomic path does
-__device__ __forceinline__ void det_add(const MlpCtx& m, const DetBufs& d, uint64_t k0, int ch, float acc) {
+__device__ __forceinline__ float* det_dst(const MlpCtx& m, const DetBufs& d, uint64_t k0, int ch) {
   const int j = (int)(k0 >> d.vbits);
   const uint64_t v = k0 & ((uint64_t(1) << d.vbits) - 1);
   const nc_grid G = grid_of(m, job_of(m, j).kind);
   if (G.grad_rows) {  // sparse gradient rows (claimed by the forward)
     const int r = G.grad_rows[v];
-    if (r >= 0) {
-      float* dst = G.grad + (int64_t)r * 32 + ch;
-      *dst = *dst + acc;
-    }
-    return;
+    return r >= 0 ? G.grad + (int64_t)r * 32 + ch : nullptr;
   }
   const int64_t H = G.dims[1], W = G.dims[2];
-  float* dst;
-  if (G.grad_stride[0] == 1 && G.grad_stride[3] == 32 && G.grad_stride[2] == 32 * W && G.grad_stride[1] == 32 * W * H) {
-    dst = G.grad + 32 * (int64_t)v + ch;  // packed channels-last gradient: row v
-  } else {
-    const int64_t x = (int64_t)(v % W), y = (int64_t)((v / W) % H), z = (int64_t)(v / (W * H));
-    dst = G.grad + z * G.grad_stride[1] + y * G.grad_stride[2] + x * G.grad_stride[3] + (int64_t)ch * G.grad_stride[0];
-  }
-  *dst = *dst + acc;
+  if (G.grad_stride[0] == 1 && G.grad_stride[3] == 32 && G.grad_stride[2] == 32 * W && G.grad_stride[1] == 32 * W * H)
+    return G.grad + 32 * (int64_t)v + ch;  // packed channels-last gradient: row v
+  const int64_t x = (int64_t)(v % W), y = (int64_t)((v / W) % H), z = (int64_t)(v / (W * H));
+  return G.grad + z * G.grad_stride[1] + y * G.grad_stride[2] + x * G.grad_stride[3] + (int64_t)ch * G.grad_stride[0];
+}
+
+__device__ __forceinline__ void det_add(const MlpCtx& m, const DetBufs& d, uint64_t k0, int ch, float acc) {
+  float* dst = det_dst(m, d, k0, ch);
+  if (dst) *dst = *dst + acc;
 }
 
 // half-wave = sub-chunk s (entries [32 s, 32 s + 32)), lane = channel.  The run sums are
@@ -159,15 +156,29 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   const K prevk = e0 > 0 ? key[e0 - 1] : invalid;
   const K nextk = e0 + cnt < n ? key[e0 + cnt] : invalid;
   float* part = d.part + s * 2 * 32 + ch;
-  for (int r = 0; r < nr; ++r) {
+  // the runs that lie inside the sub-chunk: every destination row read first (all loads in
+  // flight at once), then added to and stored -- one writer per voxel, no atomics
+  float* dst[DSUB];
+  float old[DSUB];
+#pragma unroll
+  for (int r = 0; r < DSUB; ++r) {
+    dst[r] = nullptr;
+    if (r < nr) {
+      const K k = rkey[hw][r];
+      const bool before = r == 0 && prevk == k;
+      const bool cont = r == nr - 1 && nextk == k;
+      if (k != invalid && !before && !cont) dst[r] = det_dst(m, d, (uint64_t)k, ch);
+    }
+    old[r] = dst[r] ? *dst[r] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < DSUB; ++r) {
+    if (r >= nr) break;
     const K k = rkey[hw][r];
     if (k == invalid) continue;
     const float a = racc[hw][r][ch];
-    const bool first = r == 0;
-    const bool before = first && prevk == k;
-    const bool cont = r == nr - 1 && nextk == k;
-    if (!before && !cont) det_add(m, d, (uint64_t)k, ch, a);  // the whole run is in this sub-chunk
-    else part[first ? 0 : 32] = a;
+    if (dst[r]) *dst[r] = old[r] + a;
+    else if ((r == 0 && prevk == k) || (r == nr - 1 && nextk == k)) part[r == 0 ? 0 : 32] = a;  // crosses a boundary
   }
 }
 

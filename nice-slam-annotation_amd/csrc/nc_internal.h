@@ -133,6 +133,8 @@ struct RayCtx {
   int32_t dmax_local;      // k_ray_setup reduces max(gt_depth) itself, per workgroup (small N):
                            // no k_depth_max launch
   uint32_t* range_flag;    // [MAX_JOBS] k_mlp_fwd's range flags, zeroed here (MlpCtx::range_flag)
+  int32_t lindisp;         // stratified depths linear in disparity (Renderer.py:208-209)
+  const float* t_rand;     // [N][n_strat] perturbation draws (Renderer.py:211-219), or NULL
   double bound[3][2];
   float t_strat[NC_MAX_SAMPLES];
   double t_surf[NC_MAX_SURF];

@@ -103,8 +103,13 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   if (lane < c.n_strat) {
     const float t = c.t_strat[lane];
     const float om = 1.0f - t;                               // (1.-t_vals)
-    const float nearw = has_depth ? (gd * 0.01f) * om : 0.01f * om;  // near*(1-t), float32
-    z = (double)nearw + far * (double)t;                     // + far*t (float64)
+    if (!c.lindisp) {
+      const float nearw = has_depth ? (gd * 0.01f) * om : 0.01f * om;  // near*(1-t), float32
+      z = (double)nearw + far * (double)t;                   // + far*t (float64)
+    } else {  // Renderer.py:209: 1./(1./near*(1.-t) + 1./far*t); 1./x is reciprocal(x)*1.
+      const float inv_near = has_depth ? 1.0f / (gd * 0.01f) : 100.0f;  // float32 (no depth: 1./0.01 = 100.)
+      z = 1.0 / ((double)(inv_near * om) + (1.0 / far) * (double)t);
+    }
   } else if (lane < c.n_strat + c.n_surf) {
     const double ts = c.t_surf[lane - c.n_strat];
     if (gd > 0.f) {  // Renderer.py:185-187
@@ -116,6 +121,14 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
     z = c.z_extra[r * c.n_extra + (lane - c.n_strat - c.n_surf)];
   } else {
     z = INFINITY;
+  }
+  if (c.t_rand) {  // Renderer.py:211-219: mids of neighbours, z = lower + (upper - lower) * t_rand
+    const double zp = __shfl_up(z, 1), zn = __shfl_down(z, 1);
+    if (lane < c.n_strat) {
+      const double lower = lane > 0 ? .5 * (z + zp) : z;
+      const double upper = lane < c.n_strat - 1 ? .5 * (zn + z) : z;
+      z = lower + (upper - lower) * (double)c.t_rand[r * c.n_strat + lane];
+    }
   }
 #ifdef NC_ABL_NO_SORT  // timing-only ablation: samples left unsorted
   if (false) {

@@ -22,7 +22,7 @@ def eval_points(decoders, p, c_grid, stage='middle', deterministic=None, sparse_
 
 
 def _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, n_surf,
-                       depth_max, n_importance, det):
+                       depth_max, n_importance, det, lindisp=False, t_rand=None):
     """Renderer.py:239-250: a forward-only first pass over the stratified (+ surface)
     samples, then sample_pdf over its weights without the first and last sample at the
     mid-points of its depths.  Returns the N_importance depths [N, n_importance]."""
@@ -33,7 +33,7 @@ def _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_st
     w = torch.empty(N, S, device=dev, dtype=torch.float32)
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": n_surf, "bound": bound, "depth_max": depth_max,
-            "z_out": z, "weights_out": w}
+            "z_out": z, "weights_out": w, "lindisp": lindisp, "t_rand": t_rand}
     with torch.no_grad():
         grids = [g.detach() if g is not None else None for g in _grid_args(c)]
         NiceRenderFn.apply(spec, rays_o.detach(), rays_d.detach(),
@@ -43,12 +43,28 @@ def _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_st
         return sample_pdf(z_mid, w[..., 1:-1], n_importance, det=det)
 
 
+def _t_rand(t_rand, perturb, n_rays, n_strat, device):
+    """The stratified samples' jitter draws (Renderer.py:211-219): the caller's, or -- when
+    perturb > 0 -- torch.rand([N, N_samples]) on the CPU's default generator moved to the
+    device, as the reference draws them; None when perturb == 0."""
+    if perturb <= 0. and t_rand is None:
+        return None
+    if t_rand is None:
+        t_rand = torch.rand(n_rays, n_strat)
+    t_rand = t_rand.detach().to(device=device, dtype=torch.float32).reshape(n_rays, n_strat).contiguous()
+    return t_rand
+
+
 def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_strat=32,
                 n_surf=16, depth_max=None, deterministic=None, sparse_grads=None, n_importance=0,
-                perturb=0.):
-    """Renderer.render_batch_ray core (src/utils/Renderer.py:95-262) with
-    N_importance = 0, lindisp = False, perturb = 0, occupancy = True.
+                perturb=0., lindisp=False, t_rand=None):
+    """Renderer.render_batch_ray core (src/utils/Renderer.py:95-262), occupancy = True.
     Returns (depth float64 [N], uncertainty float64 [N], color float32 [N,3]).
+
+    ``lindisp``: stratified depths linear in disparity (Renderer.py:208-209).  ``perturb``
+    > 0 jitters them inside their intervals (Renderer.py:211-219) with ``t_rand``
+    ([N, n_strat] uniform draws; default torch.rand on the CPU generator, as the
+    reference).
 
     ``depth_max``: optional device scalar replacing the batch-global max(gt_depth)
     (Renderer.py:157, :194) -- pass the all-reduced max when a batch is sharded.
@@ -69,11 +85,13 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     if n_strat + ns + n_importance > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
         raise L.NiceCoreError("nicecore supports N_samples + N_surface + N_importance <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
+    tr = _t_rand(t_rand, perturb, rays_o.shape[0], n_strat, rays_o.device)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
-            "deterministic": deterministic, "sparse": sparse_grads}
+            "deterministic": deterministic, "sparse": sparse_grads, "lindisp": bool(lindisp), "t_rand": tr}
     if n_importance > 0:
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
-                                             depth_max, n_importance, det=(perturb == 0.))
+                                             depth_max, n_importance, det=(perturb == 0.),
+                                             lindisp=bool(lindisp), t_rand=tr)
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
 
 
@@ -83,7 +101,8 @@ _LOSS_KINDS = {"mapper": L.NC_LOSS_MAPPER, "tracker": L.NC_LOSS_TRACKER}
 def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, loss="mapper",
                      target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
                      gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None,
-                     sparse_grads=None, n_importance=0, perturb=0., defer_param_grads=None):
+                     sparse_grads=None, n_importance=0, perturb=0., defer_param_grads=None, lindisp=False,
+                     t_rand=None):
     """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
     color, loss) with ``loss`` a float64 device scalar that backpropagates into the
     grids / decoders / rays like the reference's loss expression:
@@ -115,13 +134,15 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
     if n_strat + ns + n_importance > L.NC_MAX_SAMPLES or ns > L.NC_MAX_SURF:
         raise L.NiceCoreError("nicecore supports N_samples + N_surface + N_importance <= 64 (N_surface <= 32)")
     plan = make_plan(stage, decoders)
+    tr = _t_rand(t_rand, perturb, rays_o.shape[0], n_strat, rays_o.device)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
             "deterministic": deterministic, "sparse": sparse_grads,
             "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth, target_color if color_term else None),
-            "defer": defer_param_grads}
+            "defer": defer_param_grads, "lindisp": bool(lindisp), "t_rand": tr}
     if n_importance > 0:
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
-                                             depth_max, n_importance, det=(perturb == 0.))
+                                             depth_max, n_importance, det=(perturb == 0.),
+                                             lindisp=bool(lindisp), t_rand=tr)
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
 
 

@@ -429,6 +429,14 @@ class NiceRenderFn(torch.autograd.Function):
             t = spec.get(name)
             if t is not None:
                 setattr(a, name, t.data_ptr())
+        # stratified sampling options (Renderer.py:208-219): lindisp, perturb's draws
+        a.lindisp = 1 if spec.get("lindisp") else 0
+        tr = spec.get("t_rand")
+        if tr is not None:
+            if tr.dtype != torch.float32 or not tr.is_contiguous() or tuple(tr.shape) != (N, spec["n_strat"]) \
+                    or tr.device != device:
+                raise L.NiceCoreError("t_rand must be a contiguous float32 [N, n_strat] tensor on the render device")
+            a.t_rand = tr.data_ptr()
         grids = (g0, g1, g2, g3)
         gkeep = []
         for k in plan.grids:
@@ -473,7 +481,7 @@ class NiceRenderFn(torch.autograd.Function):
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
         ctx.sparse = sparse
         ctx.defer = spec.get("defer")
-        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt, zx)
+        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt, zx, tr)
         a.z_out, a.weights_out = None, None  # pass-1 outputs: not rewritten by the backward
         ctx.grids = grids
         if loss is None:

@@ -13,11 +13,13 @@ src/Tracker.py / src/Mapper.py / src/utils/Visualizer.py call it unchanged:
 plus ``render_batch_loss`` (extension): render_batch_ray with the Mapper's / Tracker's
 loss expression (Mapper.py:603-612, Tracker.py:117-131) computed in the same launches.
 
-Implemented: the NICE decoders with lindisp = False, perturb = 0, occupancy = True
-(configs/nice_slam.yaml:5,121-126) and any N_importance (hierarchical sampling,
-Renderer.py:239-259); iMAP* (slam.nice = False: one scene MLP, occupancy = False volume
-density, N_surface = 0, configs/imap.yaml) through nicecore.imap, plus its ``regulation``
-(Renderer.py:343-409); anything else raises instead of silently falling back.
+Implemented: the NICE decoders with occupancy = True (configs/nice_slam.yaml:5,121-126),
+lindisp and perturb (Renderer.py:208-219; perturb's draws are torch.rand on the CPU's
+default generator as in the reference, or the caller's ``t_rand``) and any N_importance
+(hierarchical sampling, Renderer.py:239-259); iMAP* (slam.nice = False: one scene MLP,
+occupancy = False volume density, N_surface = 0, lindisp = False, perturb = 0,
+configs/imap.yaml) through nicecore.imap, plus its ``regulation`` (Renderer.py:343-409);
+anything else raises instead of silently falling back.
 """
 from __future__ import annotations
 
@@ -47,8 +49,8 @@ class Renderer(object):
             slam.H, slam.W, slam.fx, slam.fy, slam.cx, slam.cy)
 
     def _check_supported(self):
-        if self.lindisp or self.perturb > 0.:
-            raise NotImplementedError("nicecore implements lindisp=False, perturb=0 (N_importance >= 0)")
+        if not self.nice and (self.lindisp or self.perturb > 0.):
+            raise NotImplementedError("nicecore's iMAP* path implements lindisp=False, perturb=0 (configs/imap.yaml)")
         if self.nice != self.occupancy:
             raise NotImplementedError(
                 "nicecore renders NICE decoders with occupancy=True (configs/nice_slam.yaml) and the "
@@ -80,11 +82,12 @@ class Renderer(object):
         return out
 
     def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None,
-                         depth_max=None, sparse_grads=None):
+                         depth_max=None, sparse_grads=None, t_rand=None):
         """Renderer.py:95-262.  Extensions: ``depth_max`` overrides the batch-global
         max(gt_depth) with a precomputed (e.g. all-reduced) device scalar;
         ``sparse_grads`` (nicecore.sparse.SparseGridGrads) takes the covered grids'
-        gradients as touched-voxel rows (grids too large for a dense gradient)."""
+        gradients as touched-voxel rows (grids too large for a dense gradient);
+        ``t_rand`` ([N, N_samples]) gives perturb's draws instead of torch.rand."""
         self._check_supported()
         if gt_depth is not None:
             gt_depth = gt_depth.reshape(-1)
@@ -93,12 +96,13 @@ class Renderer(object):
                                      self.N_importance, depth_max)
         return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
                            self.N_samples, self.N_surface, depth_max, sparse_grads=sparse_grads,
-                           n_importance=self.N_importance, perturb=self.perturb)
+                           n_importance=self.N_importance, perturb=self.perturb, lindisp=self.lindisp,
+                           t_rand=t_rand)
 
     def render_batch_loss(self, c, decoders, rays_d, rays_o, device, stage, gt_depth, gt_color=None,
                           loss='mapper', w_color_loss=0.2, color_term=False, handle_dynamic=False,
                           render_gt_depth='target', depth_max=None, sparse_grads=None,
-                          defer_param_grads=None):
+                          defer_param_grads=None, t_rand=None):
         """render_batch_ray + the rendering loss (ops.render_rays_loss): returns
         (depth, uncertainty, color, loss).  Mapper.optimize_map:
         ``loss='mapper', color_term=(not nice) or stage == 'color',
@@ -111,7 +115,8 @@ class Renderer(object):
                                 loss, gt_color, w_color_loss, color_term, handle_dynamic,
                                 render_gt_depth, self.N_samples, self.N_surface, depth_max,
                                 sparse_grads=sparse_grads, n_importance=self.N_importance,
-                                perturb=self.perturb, defer_param_grads=defer_param_grads)
+                                perturb=self.perturb, defer_param_grads=defer_param_grads,
+                                lindisp=self.lindisp, t_rand=t_rand)
 
     def regulation(self, c, decoders, rays_d, rays_o, gt_depth, device, stage='color', t_rand=None):
         """Renderer.py:343-409 (iMAP* only): densities of N_samples points per ray in

@@ -191,9 +191,12 @@ def eval_points(p, grids, prm, bound, dec_bounds, stage):
     return ret
 
 
-def sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf, depth_max=None):
+def sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf, depth_max=None, lindisp=False,
+                  t_rand=None):
     """Renderer.py:116-224 — z_vals [N, S] float64 (stratified + surface, sorted).
-    ``depth_max`` (sharding tests only) replaces the batch-global max(gt_depth)."""
+    ``depth_max`` (sharding tests only) replaces the batch-global max(gt_depth).
+    ``lindisp`` (Renderer.py:208-209) and ``t_rand`` (perturb > 0, :211-219: the
+    [N, n_strat] float32 draws the reference takes from torch.rand)."""
     N = rays_o.shape[0]
     if gt_depth is None:
         n_surf = 0
@@ -219,7 +222,15 @@ def sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf, depth_max=No
         zs[pos.squeeze(-1), :] = 0.95 * g * (1. - ts) + 1.05 * g * ts
         zs[~pos.squeeze(-1), :] = 0.001 * (1. - ts) + gmax * ts
     tv = torch.linspace(0., 1., steps=n_strat)
-    z = near * (1. - tv) + far * tv
+    if not lindisp:
+        z = near * (1. - tv) + far * tv
+    else:
+        z = 1. / (1. / near * (1. - tv) + 1. / far * (tv))
+    if t_rand is not None:
+        mids = .5 * (z[..., 1:] + z[..., :-1])
+        upper = torch.cat([mids, z[..., -1:]], -1)
+        lower = torch.cat([z[..., :1], mids], -1)
+        z = lower + (upper - lower) * t_rand
     if n_surf > 0:
         z, _ = torch.sort(torch.cat([z, zs.double()], -1), -1)
     return z
@@ -240,13 +251,13 @@ def composite(raw, z_vals):
 
 
 def render_batch_ray(grids, prm, dec_bounds, bound, rays_d, rays_o, stage, gt_depth=None,
-                     n_strat=32, n_surf=16, depth_max=None, n_importance=0):
-    """Renderer.py:95-262 (lindisp/perturb off, occupancy on; hierarchical sampling with
-    sample_pdf, :239-259, when n_importance > 0).
+                     n_strat=32, n_surf=16, depth_max=None, n_importance=0, lindisp=False, t_rand=None):
+    """Renderer.py:95-262 (occupancy on; lindisp, and perturb through its draws t_rand;
+    hierarchical sampling with sample_pdf, :239-259, when n_importance > 0).
     Returns (depth f64 [N], uncertainty f64 [N], color f32 [N,3])."""
     if stage == 'coarse':
         gt_depth = None
-    z = sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf, depth_max)
+    z = sample_depths(rays_o, rays_d, bound, gt_depth, n_strat, n_surf, depth_max, lindisp, t_rand)
     S = z.shape[1]
     pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
     raw = eval_points(pts.reshape(-1, 3), grids, prm, bound, dec_bounds, stage)
