@@ -391,7 +391,7 @@ def step_roofline_rays_s(stage, S, mode, fix_fine=False):
 
 
 # point-record geometry of the core (csrc/nc_mlp.hip Rec<KIND>): floats per point
-REC_STRIDE = {"coarse": 368, "middle": 464, "fine": 496, "color": 464}
+REC_STRIDE = {"coarse": 368, "middle": 368, "fine": 400, "color": 368}
 REC_LEN = {"coarse": 204, "middle": 204, "fine": 236, "color": 204}
 FEAT = {"coarse": 32, "middle": 32, "fine": 64, "color": 32}
 NOUT = {"coarse": 1, "middle": 1, "fine": 1, "color": 3}
@@ -408,7 +408,7 @@ def intermediate_bytes_per_point(stage, mode, jac=False, fix_fine=False):
     fwd = sum(4 * FEAT[d] + 16 + 4 * (REC_LEN[d] - FEAT[d]) + 4 * NOUT[d] for d in decs)
     dx = sum(32 + 4 * NOUT[d] + 16 + 16 + 24 - (1024 - 384 if jac else 0) +
              (4 * (REC_STRIDE[d] - REC_LEN[d]) if d in wdw else 0) for d in decs)
-    dw = sum(4 * REC_STRIDE[d] for d in wdw)
+    dw = sum(4 * REC_STRIDE[d] for d in wdw)  # (fourier_B's dW comes from k_mlp_dx: no dx in the record)
     gather = 128 * LOOKUPS_FWD[stage] + (384 * len(decs) if jac else 0)
     return {"k_mlp_fwd": fwd, "k_mlp_dx": dx, "k_mlp_dw": dw, "k_grid_gather": gather}
 

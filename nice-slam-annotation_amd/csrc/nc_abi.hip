@@ -161,7 +161,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 
 struct Ws {
   size_t dmax = 0, rflag = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
-         coef_d = 0, coef_c = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
+         coef_d = 0, coef_c = 0, bslab = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
          dtemp_bytes = 0,
          total = 0;
   bool det = false;
@@ -177,7 +177,10 @@ struct Ws {
   int slab_wgs = 1;        // total k_mlp_dw workgroups (= slab rows)
   int32_t dw_off[MAX_JOBS + 1] = {0, 0, 0, 0};
   int64_t slab_stride = 0;
+  int32_t bslab_rows = 0;  // k_mlp_dx workgroups per job (its grid x)
 };
+
+int fwd_grid_x(int64_t P, int n_jobs, int which);
 
 // Split `total` resident workgroups over the jobs in proportion to their per-point
 // cost (decoder MACs), each job at least 1 and at most its `blocks` work items;
@@ -275,6 +278,10 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
   w.slab_wgs = w.dw_off[pl.n_jobs];
   w.slab_stride = (max_param_count() + 63) & ~int64_t(63);
   w.slab = take((size_t)w.slab_wgs * w.slab_stride * 4);
+  if (save) {  // k_mlp_dx's Fourier-B weight-gradient rows (MlpCtx::bslab)
+    w.bslab_rows = fwd_grid_x(P, pl.n_jobs, 1);
+    w.bslab = take((size_t)pl.n_jobs * w.bslab_rows * DX_BSLAB * 4);
+  }
   if (save && vbits > 0) {  // NC_DETERMINISTIC grid-gradient buffers (nc_det.hip)
     const int64_t ne = (int64_t)pl.n_jobs * P * 8;
     w.det = true;
@@ -370,6 +377,8 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   }
   m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
   m.range_flag = at<uint32_t>(ws, w.rflag);
+  m.bslab = w.save ? at<float>(ws, w.bslab) : nullptr;
+  m.bslab_rows = w.bslab_rows;
   m.jac = w.has_jac ? at<float>(ws, w.jac) : nullptr;
 }
 
@@ -524,7 +533,7 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
   }
 }
 
-int fwd_grid_x(int64_t P, int n_jobs, int which = 0) {
+int fwd_grid_x(int64_t P, int n_jobs, int which) {
   const int64_t per = which == 0 ? FWD_THREADS / 64 * 16 * FWD_TILES : DX_THREADS / 64 * 16;
   const int64_t blocks = (P + per - 1) / per;
   int x = cu_count() * mlp_blocks_per_cu(which) / n_jobs;
@@ -550,7 +559,9 @@ int reduce_params(const MlpCtx& m, const nc_decoder_params* dec, hipStream_t s, 
 int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipStream_t s, const DetBufs* det,
                  const RayCtx* rc = nullptr, bool defer_params = false) {
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
-  if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, fwd_grid_x(P, m.n_jobs, 1), s); }), "k_mlp_dx")) return e;
+  const int dx_x = fwd_grid_x(P, m.n_jobs, 1);
+  if (m.bslab && dx_x != m.bslab_rows) return fail(-1, "nicecore: k_mlp_dx grid differs from its workspace rows");
+  if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, dx_x, s); }), "k_mlp_dx")) return e;
   bool any_grid = false;
   for (int j = 0; j < m.n_jobs; ++j) any_grid |= m.jobs[j].need_grid != 0;
   if (m.dfeat && any_grid)

@@ -374,6 +374,22 @@ __device__ __forceinline__ float fourier_cos(float x) {
   return __builtin_amdgcn_cosf(reduce_2pi(x) * 0.15915494309189535f);
 }
 
+// Sum over the 16 lanes of a DPP row (in the C layout: the 16 points i of one lane-group
+// g), left in every lane of the row: xor-1 and xor-2 quad permutes, then the half-row and
+// row mirrors.  Each step adds a lane's value to its partner's, so all 16 lanes end with
+// the same bits (fixed order, deterministic).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v = v + dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v = v + dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v = v + dpp_mov<0x141>(v);  // row_half_mirror
+  v = v + dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+
 // Wavefront reductions over the four lanes of a point (lane-groups g).
 __device__ __forceinline__ float sum_groups(float v) {
   v += __shfl_xor(v, 16);

@@ -69,6 +69,8 @@ struct MlpCtx {
   int64_t claim_cap;         // entries per shard: (waves of a job / CLAIM_SHARDS + 1) * 64
   float* dfeat;              // NC_DETERMINISTIC: [n_jobs][P][32] d features of each job's own grid
                              // (k_mlp_dx stores them instead of scattering with atomics), else NULL
+  float* bslab;              // [n_jobs][bslab_rows][DX_BSLAB] Fourier-B gradient partials, one row per
+  int32_t bslab_rows;        // k_mlp_dx workgroup (= its grid x); k_mlp_dw moves them into its slab
   uint32_t* range_flag;      // [MAX_JOBS] split-f16 range guard: k_mlp_fwd sets job j's word when
                              // an operand reached RANGE_LIMIT, k_mlp_fwd_exact then recomputes the
                              // job in f32; zeroed by k_ray_setup / k_points_prep (NULL: no guard)
@@ -205,6 +207,7 @@ struct ParamReduceCtx {
   int64_t nparam[MAX_JOBS];
   const float* slab;
 };
+constexpr int DX_BSLAB = 3 * 96;  // floats per k_mlp_dx workgroup: d B [3][EMBP]
 
 // kernels: launch wrappers (return hipError_t as int)
 int launch_depth_max(const float* gt, int64_t n, float* out, hipStream_t s);

@@ -343,8 +343,7 @@ struct Rec {
   static constexpr int PF = M + 8;           // p.float() (x, y, z, 0)
   static constexpr int LEN = PF + 4;
   static constexpr int DH = 0;
-  static constexpr int DX = 5 * HID;
-  static constexpr int DOUT = DX + (N::XYZ ? EMBP : 0);  // d loss / d output (4; unused rows 0)
+  static constexpr int DOUT = 5 * HID;       // d loss / d output (4; unused rows 0)
   static constexpr int DLEN = DOUT + 4;
   static constexpr int STRIDE = LEN + DLEN;  // one point: [forward record | backward record]
   static_assert(STRIDE % 32 == 16, "record stride must be 16 mod 32 (k_mlp_dw operand banks)");
@@ -840,7 +839,10 @@ __host__ __device__ constexpr int cmax_(int a, int b) { return a > b ? a : b; }
 constexpr int DX_SLICE_BASE = cmax_(cmax_(Net<K_COARSE, PADW_BWD>::WEIGHTS, Net<K_MID, PADW_BWD>::WEIGHTS),
                                     cmax_(Net<K_FINE, PADW_BWD>::WEIGHTS, Net<K_COLOR, PADW_BWD>::WEIGHTS));
 static_assert(DX_SLICE_BASE % 4 == 0, "scatter slices are float4-aligned");
-constexpr int DX_LDS_FLOATS = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
+// d B accumulators [wave][3][EMBP]: one private slice per wave (plain adds in a fixed
+// order, no LDS atomics), summed over the waves in wave order at the end -- deterministic
+constexpr int DX_BACC = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
+constexpr int DX_LDS_FLOATS = DX_BACC + (DX_THREADS / 64) * DX_BSLAB;
 static_assert(DX_LDS_FLOATS * 4 <= 160 * 1024, "dX LDS budget");
 
 template <int KIND, bool JAC>
@@ -853,6 +855,8 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
   const bool need_grid = job.need_grid != 0;
   const bool need_coord = job.need_coord != 0;
   const bool need_dc = need_grid || need_coord;
+  float* bacc = lds + DX_BACC + wave * DX_BSLAB;  // this wave's d fourier_B (xyz decoders, weight gradients)
+  for (int e = threadIdx.x; e < waves * DX_BSLAB; e += blockDim.x) lds[DX_BACC + e] = 0.f;  // ordered by load_weights' barrier
   load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
   float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int64_t ntiles = (ctx.P + 15) / 16;
@@ -923,10 +927,14 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
     }
     float dpf[3] = {0.f, 0.f, 0.f};
     if constexpr (N::XYZ) {
-      // dx = d emb * cos(p.float() @ B), produced 4 features at a time: stored for
-      // k_mlp_dw and reduced into d p.float() = B dx without keeping all 24 live
+      // dx = d emb * cos(p.float() @ B), produced 4 features at a time and reduced into
+      // d p.float() = B dx without keeping all 24 live.  The weight gradient of B,
+      // d B[c][m] = sum_points p.float()[c] dx[m] (decoder.py:26-30), is summed here too:
+      // over the wave's 16 points by DPP row sums, over the workgroup's tiles by LDS
+      // adds -- instead of 384 B of dx per point written to the record for k_mlp_dw.
       const float* B = lds + N::FB;
       const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
+      const float fc[3] = {f.x, f.y, f.z};
 #pragma unroll
       for (int t = 0; t < 6; ++t) {
         float dx4[4];
@@ -939,8 +947,20 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
           dpf[1] = dpf[1] + B[EMBP + m] * dx4[r];
           dpf[2] = dpf[2] + B[2 * EMBP + m] * dx4[r];
         }
-        if (need_dw && valid)
-          *reinterpret_cast<float4*>(drec + RC::DX + 16 * t + 4 * g) = float4{dx4[0], dx4[1], dx4[2], dx4[3]};
+        if (need_dw) {  // wave-uniform
+          // (c, r) = q: the row's 16-point sum of p.float()[c] * dx[16 t + 4 g + r]; lane i
+          // of the row keeps sum q = i (one live sum at a time)
+          float v = 0.f;
+#pragma unroll
+          for (int q = 0; q < 12; ++q) {
+            const float sq = row16_sum(fc[q >> 2] * dx4[q & 3]);
+            v = i == q ? sq : v;
+          }
+          if (i < 12) {  // each (c, m) of the wave belongs to one lane: plain read-add-write
+            float* a = bacc + (i >> 2) * EMBP + 16 * t + 4 * g + (i & 3);
+            *a = *a + v;
+          }
+        }
       }
       if (need_coord) {
 #pragma unroll
@@ -1012,6 +1032,17 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
       for (int k = 0; k < 3; ++k) dst[k] = gg[k] + (double)dpf[k];
     }
   }
+  if constexpr (N::XYZ) {  // this workgroup's d B partial -> its bslab row (k_mlp_dw folds the rows into its slab)
+    if (need_dw && ctx.bslab) {
+      __syncthreads();
+      float* row = ctx.bslab + ((int64_t)blockIdx.y * ctx.bslab_rows + blockIdx.x) * DX_BSLAB;
+      for (int e = threadIdx.x; e < DX_BSLAB; e += blockDim.x) {
+        float sum = 0.f;
+        for (int w = 0; w < waves; ++w) sum = sum + lds[DX_BACC + w * DX_BSLAB + e];
+        row[e] = sum;
+      }
+    }
+  }
 }
 
 // JAC: the coordinate gradient from the forward's saved Jacobian (NC_SAVE_POINT_JACOBIAN);
@@ -1076,7 +1107,8 @@ struct DwTiles {
     return ph == 0 ? 2 : ph == 1 ? 2 : ph == 2 ? NC3 : ph == 3 ? 2 : ph == 4 ? 2 : ph == 5 ? NC0 : ph <= 10 ? NCC : 1;
   }
   __host__ __device__ static constexpr int nrows(int ph) { return ph == 0 ? 1 : ph <= 10 ? 2 : 6; }
-  __host__ __device__ static constexpr bool present(int ph) { return N::XYZ || ph <= 5; }
+  // phase 11 (Fourier B) is summed by k_mlp_dx (DX_BSLAB rows), not here
+  __host__ __device__ static constexpr bool present(int ph) { return ph <= 5 || (N::XYZ && ph <= 10); }
   __host__ __device__ static constexpr int count() {
     int n = 0;
     for (int ph = 0; ph < 12; ++ph)
@@ -1108,7 +1140,7 @@ struct DwTiles {
 constexpr int DW_WAVES = DW_THREADS / 64;
 
 template <int KIND>
-__device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float* lds, int64_t wg, int64_t nwg) {
+__device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j, float* lds, int64_t wg, int64_t nwg) {
   using N = Net<KIND>;
   using RC = Rec<KIND>;
   using LY = DwLayout<KIND>;
@@ -1156,9 +1188,8 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
     } else if (ph <= 10) {
       yoff = LY::DREC + RC::DH + HID * (10 - ph) + o;
       xoff = LY::C + 16 * ti + i;
-    } else {
-      yoff = LY::DREC + RC::DX + o;
-      xoff = i < 3 ? LY::PF + i : LY::DOUT + 3;
+    } else {  // not a dW tile here (DwTiles::present)
+      yoff = xoff = LY::DOUT + 3;
     }
     if (tau >= TL::NT) yoff = xoff = LY::DOUT + 3;  // padding slot: zero operands, never flushed
     yrow[s] = g * LY::RS + yoff;
@@ -1305,6 +1336,17 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, float*
     const int64_t bi = PhaseMap<KIND>::b_index(ph, row);
     if (bi >= 0) slab[bi] = bacc[e];
   }
+  if constexpr (N::XYZ) {  // fourier_B: k_mlp_dx's per-workgroup rows wg, wg + nwg, ... summed in order
+    if (ctx.bslab) {
+      const float* bs = ctx.bslab + (int64_t)j * ctx.bslab_rows * DX_BSLAB;
+      for (int e = threadIdx.x; e < 3 * EMB; e += blockDim.x) {
+        const int c = e / EMB, m = e - c * EMB;
+        float sum = 0.f;
+        for (int64_t r = wg; r < ctx.bslab_rows; r += nwg) sum = sum + bs[r * DX_BSLAB + c * EMBP + m];
+        slab[N::P_B + e] = sum;
+      }
+    }
+  }
 }
 
 __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
@@ -1316,10 +1358,10 @@ __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
   const int o0 = j == 0 ? ctx.dw_off[0] : (j == 1 ? ctx.dw_off[1] : ctx.dw_off[2]);
   const int o1 = j == 0 ? ctx.dw_off[1] : (j == 1 ? ctx.dw_off[2] : ctx.dw_off[3]);
   switch (job.kind) {
-    case K_COARSE: dw_job<K_COARSE>(ctx, job, lds, b - o0, o1 - o0); break;
-    case K_MID: dw_job<K_MID>(ctx, job, lds, b - o0, o1 - o0); break;
-    case K_FINE: dw_job<K_FINE>(ctx, job, lds, b - o0, o1 - o0); break;
-    default: dw_job<K_COLOR>(ctx, job, lds, b - o0, o1 - o0); break;
+    case K_COARSE: dw_job<K_COARSE>(ctx, job, j, lds, b - o0, o1 - o0); break;
+    case K_MID: dw_job<K_MID>(ctx, job, j, lds, b - o0, o1 - o0); break;
+    case K_FINE: dw_job<K_FINE>(ctx, job, j, lds, b - o0, o1 - o0); break;
+    default: dw_job<K_COLOR>(ctx, job, j, lds, b - o0, o1 - o0); break;
   }
 }
 
