@@ -1071,9 +1071,9 @@ __global__ void __launch_bounds__(DX_THREADS) k_mlp_dx(const MlpCtx ctx) {
 // per workgroup into a slab, summed by k_param_reduce.
 // ---------------------------------------------------------------------------
 #ifndef NC_DW_NPTS
-#define NC_DW_NPTS 32
+#define NC_DW_NPTS 16
 #endif
-constexpr int DW_NPTS = NC_DW_NPTS;  // points per staged sub-chunk (8 MFMA k-steps)
+constexpr int DW_NPTS = NC_DW_NPTS;  // points per staged sub-chunk (4 MFMA k-steps; 16 vs 32: dw -2.5 us at C2 with the 656-B backward record, profiles/r03/ab_dw_shapes.log)
 
 template <int KIND>
 struct DwLayout {

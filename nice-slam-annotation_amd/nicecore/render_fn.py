@@ -308,12 +308,22 @@ def _bind_sparse(sparse, args, plan, n_points=None):
                 sparse.bind_forward(args.grids[k], k, n_points)
 
 
+_PARAM_COUNT = {}  # decoder kind -> nc_param_count (a constant of the library)
+
+
+def _param_count(lib, k):
+    n = _PARAM_COUNT.get(k)
+    if n is None:
+        n = _PARAM_COUNT[k] = int(lib.nc_param_count(k))
+    return n
+
+
 def _grad_sizes(lib, plan, needs_params, needs_grids, grids):
     sl = plan.param_slices()
     gk = [k for k in plan.grids if needs_grids[k]]
     pk = [k for k in plan.decs if any(needs_params[sl[k][0]:sl[k][1]])]
     gsize = sum(grids[k].numel() for k in gk)
-    psize = {k: int(lib.nc_param_count(k)) for k in pk}
+    psize = {k: _param_count(lib, k) for k in pk}
     return gk, pk, gsize, psize
 
 

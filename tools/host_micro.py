@@ -15,15 +15,19 @@ import torch  # noqa: E402
 
 
 def per_call(fn, n=400):
+    """Host time of one call: each call timed alone with the device idle (synchronised
+    before it), so a backed-up launch queue cannot stall the measured enqueue."""
     for _ in range(20):
         fn()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    tot = 0.0
     for _ in range(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         fn()
-    t1 = time.perf_counter()
+        tot += time.perf_counter() - t0
     torch.cuda.synchronize()
-    return 1e6 * (t1 - t0) / n
+    return 1e6 * tot / n
 
 
 if __name__ == "__main__":
