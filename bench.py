@@ -91,6 +91,10 @@ def parse():
                     help="render with the loss target as gt_depth (Mapper / Tracker, S = 48) or "
                          "without one (S = 32: BASELINE configs[0], the reference's CPU plumbing "
                          "case C1; the loss still compares with the targets)")
+    ap.add_argument("--param-grads", default="autograd", choices=["autograd", "direct"],
+                    help="how the decoder parameters get .grad in the drop-in step (render_fn.param_inputs): "
+                         "through autograd (default, what the unmodified Mapper/Tracker run) or written by the "
+                         "backward itself (opt-in rendering.param_grads: direct); both eager times are reported")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -194,7 +198,7 @@ def build_workload(args, rank, device, world=1):
     ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000 + rank)
     slam = types.SimpleNamespace(nice=True, bound=sc.bound, H=sc.H, W=sc.W, fx=sc.fx, fy=sc.fy,
                                  cx=sc.cx, cy=sc.cy)
-    cfg = {"rendering": dict(S.DEFAULT_RENDERING), "scale": 1, "occupancy": True}
+    cfg = {"rendering": dict(S.DEFAULT_RENDERING, param_grads=args.param_grads), "scale": 1, "occupancy": True}
     renderer = Renderer(cfg, None, slam)
     ba = args.mode == "ba"
     for g in grids.values():
@@ -551,6 +555,18 @@ def main():
         eager()
     torch.cuda.synchronize()
     eager_ms = 1e3 * (time.perf_counter() - t0) / max(5, min(args.steps, 20))
+    # the same eager step with the other parameter-gradient mode (reported beside it)
+    other = "direct" if args.param_grads == "autograd" else "autograd"
+    w["renderer"].param_grads = other
+    for _ in range(3):
+        eager()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(max(5, min(args.steps, 20))):
+        eager()
+    torch.cuda.synchronize()
+    eager_other_ms = 1e3 * (time.perf_counter() - t0) / max(5, min(args.steps, 20))
+    w["renderer"].param_grads = args.param_grads
 
     step = graphed if graphed is not None else eager
     for _ in range(args.warmup):
@@ -650,6 +666,8 @@ def main():
                           "note": "SURVEY.md §8(d): min(157.3 TF / FLOP per ray, 8 TB/s / bytes per ray)"},
         "launch": "hipGraph replay" if graphed is not None else "eager",
         "eager_ms_per_step": round(eager_ms, 4),
+        "param_grads": args.param_grads,
+        f"eager_{other}_ms_per_step": round(eager_other_ms, 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1])},
     }
     if args.iteration and world == 1 and w["ba"] and w["sparse"] is None:

@@ -223,6 +223,16 @@ def load(path: str | None = None):
     return lib
 
 
+def raw_stream(device) -> int:
+    """hipStream_t of torch's current stream on ``device`` (the value of
+    torch.cuda.current_stream(device).cuda_stream, without building the stream object)."""
+    import torch
+    if not isinstance(device, torch.device):
+        device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
+
+
 def check(rc: int, what: str):
     if rc != 0:
         msg = load().nc_last_error()

@@ -53,26 +53,32 @@ def _dense(t):
 
 def _shared_bases(grads):
     """Split grads into (flat 1-D ranges to reduce, remaining grads).  The render core
-    puts every gradient of one backward call into one buffer (render_fn._alloc_grads:
+    puts every gradient of one backward call into one buffer (render_fn._GradBuffer:
     grid gradients first, then the decoder parameters), each gradient a dense view of
     a contiguous range of it; gradients whose ranges tile a stretch of the buffer
     without gaps are reduced as that one 1-D range (a single collective, and no
-    channels-last views handed to the backend)."""
-    by_base = {}
+    channels-last views handed to the backend).
+
+    Grouped by STORAGE, not by ``._base``: AccumulateGrad stores a detached alias of
+    the gradient it steals, which keeps the storage but not the view's base.  A
+    contiguous gradient that is its whole storage (an ordinary one) stays apart."""
+    by_store = {}
     rest = []
     for g in grads:
-        b = g._base
-        if b is not None and b.is_contiguous() and b.dtype == g.dtype and _dense(g):
-            off = g.storage_offset() - b.storage_offset()
-            by_base.setdefault(id(b), (b, []))[1].append((off, off + g.numel(), g))
-        else:
+        st = g.untyped_storage()
+        whole = g.storage_offset() == 0 and g.numel() * g.element_size() == st.nbytes()
+        if (whole and g.is_contiguous()) or not _dense(g):
             rest.append(g)
+            continue
+        off = g.storage_offset()
+        by_store.setdefault((st.data_ptr(), g.dtype, g.device), (g, []))[1].append((off, off + g.numel()))
     ranges = []
-    for b, spans in by_base.values():
-        spans.sort(key=lambda x: x[0])
-        flat = b.reshape(-1)
-        lo, hi = spans[0][0], spans[0][1]
-        for s0, s1, _ in spans[1:]:
+    for g0, spans in by_store.values():
+        st = g0.untyped_storage()
+        flat = torch.empty(0, dtype=g0.dtype, device=g0.device).set_(st, 0, (st.nbytes() // g0.element_size(),))
+        spans.sort()
+        lo, hi = spans[0]
+        for s0, s1 in spans[1:]:
             if s0 == hi:
                 hi = s1
             else:

@@ -83,7 +83,7 @@ class FrustumSelector:
             self._scratch = torch.zeros(1, dtype=torch.int32, device=self.device)
         a.mask = mask.data_ptr()
         a.scratch = self._scratch.data_ptr()
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        stream = L.raw_stream(self.device)
         L.check(lib.nc_frustum_mask(ctypes.byref(a), stream), "nc_frustum_mask")
         self._keep = depth_t
         return mask
@@ -111,7 +111,7 @@ def _rows_call(op, grid, rows, packed):
     for k in range(4):
         a.stride[k] = grid.stride(1 + k)
     a.packed = packed.data_ptr() if packed is not None else None
-    L.check(lib.nc_grid_rows(ctypes.byref(a), torch.cuda.current_stream(grid.device).cuda_stream), "nc_grid_rows")
+    L.check(lib.nc_grid_rows(ctypes.byref(a), L.raw_stream(grid.device)), "nc_grid_rows")
 
 
 class _RowsScatter(torch.autograd.Function):

@@ -119,7 +119,7 @@ class ImapRenderFn(torch.autograd.Function):
         if nbytes == 0:
             L.check(-1, "nc_imap_render_workspace_bytes")
         ws = torch.empty(nbytes, device=device, dtype=torch.uint8)
-        stream = torch.cuda.current_stream(device).cuda_stream
+        stream = L.raw_stream(device)
         L.check(lib.nc_imap_render_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_imap_render_forward")
         a.z_out, a.weights_out = None, None
         ctx.args, ctx.ws, ctx.nbytes = a, ws, nbytes
@@ -148,7 +148,7 @@ class ImapRenderFn(torch.autograd.Function):
             flat = torch.zeros(lib.nc_imap_param_count(), device=device, dtype=torch.float32)
             a.dec.grad = flat.data_ptr()
         if rays_o.shape[0] > 0:
-            stream = torch.cuda.current_stream(device).cuda_stream
+            stream = L.raw_stream(device)
             L.check(lib.nc_imap_render_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
                     "nc_imap_render_backward")
         elif g_ro is not None:
@@ -179,7 +179,7 @@ class ImapEvalFn(torch.autograd.Function):
         a.raw = raw.data_ptr()
         nbytes = lib.nc_imap_points_workspace_bytes(ctypes.byref(a))
         ws = torch.empty(max(nbytes, 1), device=device, dtype=torch.uint8)
-        stream = torch.cuda.current_stream(device).cuda_stream
+        stream = L.raw_stream(device)
         L.check(lib.nc_imap_points_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_imap_points_forward")
         ctx.args, ctx.ws, ctx.nbytes = a, ws, nbytes
         ctx.keep = (pts, params)
@@ -202,7 +202,7 @@ class ImapEvalFn(torch.autograd.Function):
             flat = torch.zeros(lib.nc_imap_param_count(), device=device, dtype=torch.float32)
             a.dec.grad = flat.data_ptr()
         if a.n_points > 0:
-            stream = torch.cuda.current_stream(device).cuda_stream
+            stream = L.raw_stream(device)
             L.check(lib.nc_imap_points_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
                     "nc_imap_points_backward")
         a.dec.grad = None

@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib as L
-from .render_fn import NiceEvalFn, NiceRenderFn, make_plan
+from .render_fn import NiceEvalFn, NiceRenderFn, make_plan, param_inputs
 
 
 def _grid_args(c):
@@ -57,7 +57,7 @@ def _t_rand(t_rand, perturb, n_rays, n_strat, device):
 
 def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_strat=32,
                 n_surf=16, depth_max=None, deterministic=None, sparse_grads=None, n_importance=0,
-                perturb=0., lindisp=False, t_rand=None):
+                perturb=0., lindisp=False, t_rand=None, param_grads=None):
     """Renderer.render_batch_ray core (src/utils/Renderer.py:95-262), occupancy = True.
     Returns (depth float64 [N], uncertainty float64 [N], color float32 [N,3]).
 
@@ -78,7 +78,10 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
 
     ``n_importance`` > 0: hierarchical sampling (Renderer.py:239-259) -- a forward-only
     pass, ``sample_pdf`` (deterministic u when ``perturb`` == 0, as the reference), and
-    the differentiable render over the sorted union of both sample sets."""
+    the differentiable render over the sorted union of both sample sets.
+
+    ``param_grads``: "autograd" (default) or "direct" -- how the decoder parameters get
+    their ``.grad`` (render_fn.param_inputs)."""
     if stage == 'coarse':
         gt_depth = None
     ns = n_surf if gt_depth is not None else 0
@@ -92,7 +95,8 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
                                              depth_max, n_importance, det=(perturb == 0.),
                                              lindisp=bool(lindisp), t_rand=tr)
-    return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
+    return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c),
+                              *param_inputs(spec, plan, rays_o.device, param_grads))
 
 
 _LOSS_KINDS = {"mapper": L.NC_LOSS_MAPPER, "tracker": L.NC_LOSS_TRACKER}
@@ -102,7 +106,7 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
                      target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
                      gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None,
                      sparse_grads=None, n_importance=0, perturb=0., defer_param_grads=None, lindisp=False,
-                     t_rand=None):
+                     t_rand=None, param_grads=None):
     """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
     color, loss) with ``loss`` a float64 device scalar that backpropagates into the
     grids / decoders / rays like the reference's loss expression:
@@ -118,7 +122,8 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
     use_color_in_tracking).  ``gt_depth`` is the depth that guides the surface samples;
     by default the target itself (the tracker and the non-coarse mapper); the coarse
     mapper renders with None.  ``defer_param_grads``: a render_fn.DeferParamGrads that
-    takes the decoder weight gradients out of ``backward()`` (data-parallel overlap)."""
+    takes the decoder weight gradients out of ``backward()`` (data-parallel overlap).
+    ``param_grads``: see render_rays."""
     if loss not in _LOSS_KINDS:
         raise L.NiceCoreError(f"loss must be one of {sorted(_LOSS_KINDS)}")
     if handle_dynamic and loss != "tracker":
@@ -143,7 +148,8 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
                                              depth_max, n_importance, det=(perturb == 0.),
                                              lindisp=bool(lindisp), t_rand=tr)
-    return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c), *plan.flat_params())
+    return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c),
+                              *param_inputs(spec, plan, rays_o.device, param_grads))
 
 
 def sample_pdf(bins, weights, N_samples, det=False, device=None, u=None):
@@ -175,5 +181,5 @@ def sample_pdf(bins, weights, N_samples, det=False, device=None, u=None):
                     n_samples=N_samples, bins=b.data_ptr(), bins_stride=nb, weights=w.data_ptr(),
                     weights_stride=nb - 1, u=uu.data_ptr() if uu is not None else None,
                     u_stride=N_samples, samples=out.data_ptr(), samples_stride=N_samples)
-    L.check(lib.nc_sample_pdf(ctypes.byref(a), torch.cuda.current_stream(dev).cuda_stream), "nc_sample_pdf")
+    L.check(lib.nc_sample_pdf(ctypes.byref(a), L.raw_stream(dev)), "nc_sample_pdf")
     return out.reshape(*lead, N_samples)

@@ -65,7 +65,7 @@ def adam_step_(param, grad, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weigh
     a = _adam_args(L.NC_ADAM_DENSE, lr, beta1, beta2, eps, weight_decay, step)
     a.n = param.numel()
     a.param, a.grad, a.exp_avg, a.exp_avg_sq = (t.data_ptr() for t in ts)
-    stream = torch.cuda.current_stream(param.device).cuda_stream
+    stream = L.raw_stream(param.device)
     L.check(L.load().nc_adam_step(ctypes.byref(a), stream), "nc_adam_step")
 
 
@@ -132,7 +132,7 @@ class Adam(torch.optim.Optimizer):
         """All segments in one nc_adam_step_multi call (one launch per 32 parameters)."""
         arr = (L.NcAdamSegment * len(segs))(*[L.NcAdamSegment(*s) for s in segs])
         a = _adam_args(L.NC_ADAM_DENSE, 0.0, betas[0], betas[1], eps, 0.0, 1.0)
-        stream = torch.cuda.current_stream(device).cuda_stream
+        stream = L.raw_stream(device)
         L.check(L.load().nc_adam_step_multi(ctypes.byref(a), arr, len(segs), stream), "nc_adam_step_multi")
 
 
@@ -171,7 +171,7 @@ class SparseGridAdam:
             a.exp_avg, a.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
             a.row_voxel, a.row_count, a.row_capacity = r.row_voxel.data_ptr(), r.count.data_ptr(), r.capacity
             a.voxel_stride, a.channel_stride = g.stride(4), g.stride(1)
-            stream = torch.cuda.current_stream(g.device).cuda_stream
+            stream = L.raw_stream(g.device)
             L.check(lib.nc_adam_step(ctypes.byref(a), stream), "nc_adam_step")
 
 
@@ -256,7 +256,7 @@ class ShardedSparseGridAdam:
             a.exp_avg_sq = st["exp_avg_sq"].data_ptr() - v0 * 32 * 4
             a.row_voxel, a.row_count, a.row_capacity = my_vox.data_ptr(), cnt.data_ptr(), own
             a.voxel_stride, a.channel_stride = 32, 1
-            stream = torch.cuda.current_stream(g.device).cuda_stream
+            stream = L.raw_stream(g.device)
             L.check(lib.nc_adam_step(ctypes.byref(a), stream), "nc_adam_step")
             if world == 1:
                 continue

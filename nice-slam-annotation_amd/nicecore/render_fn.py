@@ -15,6 +15,7 @@ gradient and grid scatter).
 from __future__ import annotations
 
 import ctypes
+import operator
 import os
 import weakref
 
@@ -27,7 +28,12 @@ def _ptr(t):
     return t.data_ptr() if t is not None else None
 
 
+_data_ptr = torch.Tensor.data_ptr
+
+
 _unflatten = torch._C._nn.unflatten_dense_tensors  # flat, tensors -> views shaped like tensors
+
+_stream = L.raw_stream
 
 
 def _bound_rows(b) -> list:
@@ -139,6 +145,28 @@ def _fill_grid(ng: L.NcGrid, t, device):
         ng.grad_stride[a] = st[1 + a]
 
 
+_NCGRID_BYTES = ctypes.sizeof(L.NcGrid)
+
+
+def _fill_grid_cached(ng: L.NcGrid, t, device):
+    """_fill_grid through an image cached ON the caller's grid tensor, tagged with its
+    storage pointer, strides, shape, dtype and device (the per-call checks and ~15 ctypes
+    field writes become one tag compare and one memmove)."""
+    tag = (t.data_ptr(), t.stride(), t.shape, t.dtype, t.device)
+    hit = getattr(t, "_nicecore_grid", None)
+    if hit is None or hit[0] != tag:
+        img = L.NcGrid()
+        _fill_grid(img, t, device)
+        hit = (tag, img)
+        try:
+            t._nicecore_grid = hit
+        except (AttributeError, RuntimeError):
+            pass
+    elif t.device != device:
+        raise L.NiceCoreError(f"feature grid must be float32 on {device}")
+    ctypes.memmove(ctypes.addressof(ng), ctypes.addressof(hit[1]), _NCGRID_BYTES)
+
+
 def _decoder_bound(module, name):
     b = getattr(module, "bound", None)
     if b is None:
@@ -200,6 +228,7 @@ class _Plan:
         self._sig = None
         self._dec_img = None
         self._templates = {}
+        self.grad_pool = {}  # _GradBuffer entries kept for reuse (see _GradBuffer)
 
     def flat_params(self):
         return list(self._flat)
@@ -212,7 +241,7 @@ class _Plan:
         for k in self.decs:
             b = self.bounds[k]
             bt.append((b.data_ptr(), b._version) if isinstance(b, torch.Tensor) else id(b))
-        return tuple(p.data_ptr() for p in self._flat), tuple(bt)
+        return tuple(map(_data_ptr, self._flat)), tuple(bt)
 
     def still_valid(self, decoders) -> bool:
         mods = decoder_modules(decoders)
@@ -327,68 +356,143 @@ def _grad_sizes(lib, plan, needs_params, needs_grids, grids):
     return gk, pk, gsize, psize
 
 
-def _alloc_grads(lib, plan, needs_params, needs_grids, grids, args, device, prezeroed=None, sparse=None):
-    """Every gradient of one backward call lives in ONE float32 buffer: the grid
-    gradients first (strided views with each grid's own memory format, zero-filled
-    by a single kernel), then one flat parameter vector per decoder whose
-    parameters need a gradient (written, not accumulated, by the library).  The
-    views are stolen by AccumulateGrad as the leaves' .grad (their strides obey
-    the layout contract), and distributed.allreduce_grads reduces the shared
-    buffer with one collective."""
+class _GradBuffer:
+    """Every gradient of one backward call in ONE float32 buffer: the grid gradients
+    first (strided views with each grid's own memory format, zero-filled by a single
+    kernel), then one flat parameter vector per decoder whose parameters need a
+    gradient (written, not accumulated, by the library), and the per-parameter
+    views of those vectors.  The backward hands out detached aliases of the views:
+    AccumulateGrad steals them as the leaves' .grad (their strides obey the layout
+    contract) and distributed.allreduce_grads reduces the shared buffer with one
+    collective.
+
+    The buffer and its views are kept for reuse (``_grad_buffer``): once nothing
+    outside the entry references its storage any more (the caller set the .grad of
+    the last step to None, Mapper.py:620 / Tracker.py:135 ``zero_grad``), the next
+    call takes the same buffer and views instead of building ~80 new views (the
+    host cost of the drop-in path).  Entries are per (plan, stream, gradient set),
+    so reuse is stream-ordered like the caching allocator's, and never used inside a
+    stream capture (memory captured into a graph stays in the graph's pool)."""
+
+    __slots__ = ("key", "buf", "gsize", "grid_grads", "flats", "pviews", "base")
+
+    def __init__(self, key, plan, pk, gk, gsize, psize, grids, device):
+        self.key, self.gsize = key, gsize
+        self.buf = buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
+        self.grid_grads = [None] * 4
+        off = 0
+        for k in gk:
+            g = grids[k]
+            self.grid_grads[k] = torch.as_strided(buf, g.shape, _dense_strides(g), off)
+            off += g.numel()
+        self.flats = {}
+        self.pviews = []
+        for k in plan.decs:
+            ps = plan.params[k]
+            if k in psize:
+                self.flats[k] = f = buf[off:off + psize[k]]
+                off += psize[k]
+                self.pviews += _unflatten(f, ps)
+            else:
+                self.pviews += [None] * len(ps)
+        self.base = _use_count(buf)
+
+    def free(self):
+        return _use_count(self.buf) == self.base
+
+    def bind(self, args, plan, sparse):
+        for k in plan.grids:
+            args.grids[k].grad = None
+            args.grids[k].grad_rows = None
+        _bind_sparse(sparse, args, plan)
+        for k, gg in enumerate(self.grid_grads):
+            if gg is not None:
+                args.grids[k].grad = gg.data_ptr()
+                st = gg.stride()
+                for ax in range(4):
+                    args.grids[k].grad_stride[ax] = st[1 + ax]
+        for k in plan.decs:
+            args.dec[k].grad = None
+        for k, f in self.flats.items():
+            args.dec[k].grad = f.data_ptr()
+
+    def outputs(self, needs_params):
+        """(grid gradients, parameter gradients) as fresh aliases (None where not needed)."""
+        gg = [g.detach() if g is not None else None for g in self.grid_grads]
+        pg = [v.detach() if (v is not None and n) else None for v, n in zip(self.pviews, needs_params)]
+        return gg, pg
+
+    def zero(self):
+        self.buf.zero_()
+
+
+def _use_count(t):
+    return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
+
+
+def _grad_buffer(lib, plan, needs_params, needs_grids, grids, device, stream):
+    """The _GradBuffer for one backward call: a free pooled one with the same layout
+    when there is one, else a new one.  Returns (entry, fresh)."""
     gk, pk, gsize, psize = _grad_sizes(lib, plan, needs_params, needs_grids, grids)
-    if prezeroed is not None and prezeroed.numel() == gsize + sum(psize.values()):
-        buf = prezeroed  # grid part zero-filled by the forward (nc_render_args.grad_zero)
-    else:
-        buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
-        if gsize:
-            buf[:gsize].zero_()
-    grid_grads = [None] * 4
-    off = 0
-    for k in plan.grids:
-        args.grids[k].grad = None
-        args.grids[k].grad_rows = None
-    _bind_sparse(sparse, args, plan)
-    for k in gk:
-        g = grids[k]
-        gg = torch.as_strided(buf, g.shape, _dense_strides(g), off)
-        args.grids[k].grad = gg.data_ptr()
-        st = gg.stride()
-        for ax in range(4):
-            args.grids[k].grad_stride[ax] = st[1 + ax]
-        grid_grads[k] = gg
-        off += g.numel()
-    flats = {}
-    for k in plan.decs:
-        args.dec[k].grad = None
-    for k in pk:
-        flats[k] = buf[off:off + psize[k]]
-        args.dec[k].grad = flats[k].data_ptr()
-        off += psize[k]
-    return grid_grads, flats
+    if torch.cuda.is_current_stream_capturing():
+        return _GradBuffer(None, plan, pk, gk, gsize, psize, grids, device), True
+    key = (stream, tuple(gk), tuple(pk), tuple((grids[k].shape, _dense_strides(grids[k])) for k in gk))
+    pool = plan.grad_pool
+    e = pool.pop(key, None)
+    if e is not None and e.free():
+        return e, False
+    return _GradBuffer(key, plan, pk, gk, gsize, psize, grids, device), True
 
 
-def _zero_grads(grid_grads, flats):
-    for g in grid_grads:
-        if g is not None:
-            g.zero_()
-    for f in flats.values():
-        f.zero_()
+def _release(plan, entry):
+    if entry is not None and entry.key is not None:
+        plan.grad_pool[entry.key] = entry
 
 
-def _split_param_grads(plan, flats, needs_params):
-    """Per-parameter views of each decoder's flat gradient (one C++ call per decoder:
-    unflatten_dense_tensors, instead of a slice + view per parameter in Python)."""
-    out = []
-    sl = plan.param_slices()
-    for k in plan.decs:
-        a, b = sl[k]
-        ps = plan.params[k]
-        if k not in flats:
-            out += [None] * len(ps)
-            continue
-        views = _unflatten(flats[k], ps)
-        out += [v if needs_params[a + j] else None for j, v in enumerate(views)]
-    return out
+PARAM_GRAD_MODES = ("autograd", "direct")
+# default for render_rays / render_rays_loss / Renderer when the caller does not choose
+_PARAM_GRADS = os.environ.get("NICECORE_PARAM_GRADS", "autograd")
+_requires_grad = operator.attrgetter("requires_grad")
+_ANCHORS = {}  # device -> zero-size leaf that connects a "direct" render to the graph
+
+
+def param_inputs(spec, plan, device, mode=None):
+    """The decoder-parameter inputs of NiceRenderFn.
+
+    ``"autograd"`` (default): the parameters themselves, so their gradients reach
+    ``.grad`` through AccumulateGrad like any autograd leaf (hooks, autograd.grad,
+    DDP all see them).
+    ``"direct"`` (opt-in: ``rendering: {param_grads: direct}`` in the config, or
+    ``NICECORE_PARAM_GRADS=direct``): the parameters stay out of the autograd graph
+    and the backward writes their ``.grad`` itself -- set when None, added otherwise,
+    the values AccumulateGrad would give.  One zero-size anchor leaf stands in for
+    them, so ~80 AccumulateGrad nodes and Function inputs per call disappear from the
+    host path (the Mapper's loss.backward(); optimizer.step() loop, Mapper.py:598-625,
+    sees the same .grad).  Not for callers that hook the decoder parameters or take
+    their gradients with torch.autograd.grad."""
+    mode = mode or _PARAM_GRADS
+    if mode == "autograd":
+        return plan._flat
+    if mode != "direct":
+        raise L.NiceCoreError(f"param_grads must be one of {PARAM_GRAD_MODES}, got {mode!r}")
+    flat = plan._flat
+    needs = tuple(map(_requires_grad, flat)) if torch.is_grad_enabled() else (False,) * len(flat)
+    spec["param_needs"], spec["direct_params"] = needs, flat
+    if not any(needs):
+        return ()
+    a = _ANCHORS.get(device)
+    if a is None:
+        a = _ANCHORS[device] = torch.empty(0, device=device, requires_grad=True)
+    return (a,)
+
+
+def _attach(pairs):
+    """AccumulateGrad's effect for the direct mode: .grad set when None, else added."""
+    for p, g in pairs:
+        if p.grad is None:
+            p.grad = g
+        else:
+            p.grad.add_(g)
 
 
 class NiceRenderFn(torch.autograd.Function):
@@ -413,10 +517,18 @@ class NiceRenderFn(torch.autograd.Function):
         a = L.NcRenderArgs.from_buffer_copy(
             plan.render_template(device, spec["n_strat"], spec["n_surf"], spec["bound"]))
         a.flags = _flags(ctx, spec, (1, 2))
+        pneeds = spec.get("param_needs")  # "direct" parameter gradients (param_inputs)
+        ctx.direct = pneeds is not None
+        ctx.n_param_inputs = len(params)
+        if pneeds is None:
+            pneeds = ctx.needs_input_grad[8:]
+        else:
+            params = spec["direct_params"]
+        ctx.pneeds = pneeds
         if a.flags & L.NC_SAVE_FOR_BACKWARD:  # decoders without a weight gradient: no activation records
             sl = plan.param_slices()
             for k in plan.decs:
-                if not any(ctx.needs_input_grad[8 + sl[k][0]:8 + sl[k][1]]):
+                if not any(pneeds[sl[k][0]:sl[k][1]]):
                     a.flags |= L.NC_NO_WEIGHT_GRAD(k)
         a.n_rays = N
         a.rays_o = rays_o.data_ptr()
@@ -452,9 +564,8 @@ class NiceRenderFn(torch.autograd.Function):
         for k in plan.grids:
             if grids[k] is None:
                 raise L.NiceCoreError(f"stage needs {L.GRID_KEYS[k]}")
-            g = grids[k].detach()
-            _fill_grid(a.grids[k], g, device)
-            gkeep.append(g)
+            _fill_grid_cached(a.grids[k], grids[k], device)
+            gkeep.append(grids[k].detach())
         if a.flags & L.NC_SAVE_FOR_BACKWARD:
             _bind_sparse(sparse, a, plan, N * (spec["n_strat"] + spec["n_surf"] + a.n_extra))
         depth = torch.empty(N, device=device, dtype=torch.float64)
@@ -472,20 +583,22 @@ class NiceRenderFn(torch.autograd.Function):
             loss = torch.empty((), device=device, dtype=torch.float64)
             a.loss, a.loss_flags, a.w_color = kind, lflags, float(w)
             a.loss_depth, a.loss_color, a.loss_out = tgt[0].data_ptr(), _ptr(tgt[1]), loss.data_ptr()
-        # the backward's gradient buffer: allocated here and zero-filled by the forward's
-        # gather kernel (no separate fill launch); used by the first backward call
-        ctx.grad_buf = None
+        # the backward's gradient buffer: taken here and its grid part zero-filled by the
+        # forward's gather kernel (no separate fill launch); used by the first backward call
+        ctx.grad_entry = None
+        stream = _stream(device)
         dneeds = _dense_needs(ctx.needs_input_grad[4:8], sparse)
         if _FWD_ZERO and any(dneeds):
-            _, _, gsize, psize = _grad_sizes(lib, plan, ctx.needs_input_grad[8:], dneeds, (g0, g1, g2, g3))
-            if gsize:
-                ctx.grad_buf = torch.empty(gsize + sum(psize.values()), device=device, dtype=torch.float32)
-                a.grad_zero, a.grad_zero_floats = ctx.grad_buf.data_ptr(), gsize
+            e, _ = _grad_buffer(lib, plan, pneeds, dneeds, grids, device, stream)
+            if e.gsize:
+                ctx.grad_entry = e
+                a.grad_zero, a.grad_zero_floats = e.buf.data_ptr(), e.gsize
+            else:
+                _release(plan, e)
         nbytes = lib.nc_render_workspace_bytes(ctypes.byref(a))
         if nbytes == 0:
             L.check(-1, "nc_render_workspace_bytes")
         ws = torch.empty(nbytes, device=device, dtype=torch.uint8)
-        stream = torch.cuda.current_stream(device).cuda_stream
         L.check(lib.nc_render_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_render_forward")
         a.grad_zero, a.grad_zero_floats = None, 0
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
@@ -518,15 +631,22 @@ class NiceRenderFn(torch.autograd.Function):
             g_ro = g_ro if g_ro is not None else torch.empty_like(rays_o)
             g_rd = g_rd if g_rd is not None else torch.empty_like(rays_o)
         a.g_rays_o, a.g_rays_d = _ptr(g_ro), _ptr(g_rd)
-        needs_params = need[8:]
-        grid_grads, flats = _alloc_grads(lib, plan, needs_params, _dense_needs(need[4:8], ctx.sparse), ctx.grids,
-                                         a, device, prezeroed=ctx.grad_buf, sparse=ctx.sparse)
-        ctx.grad_buf = None  # a second backward (retain_graph) gets a fresh, zeroed buffer
+        needs_params = ctx.pneeds
+        stream = _stream(device)
+        e = ctx.grad_entry
+        ctx.grad_entry = None  # a second backward (retain_graph) gets a fresh, zeroed buffer
+        if e is None:
+            e, _ = _grad_buffer(lib, plan, needs_params, _dense_needs(need[4:8], ctx.sparse), ctx.grids,
+                                device, stream)
+            if e.gsize:
+                e.buf[:e.gsize].zero_()
+        e.bind(a, plan, ctx.sparse)
         if rays_o.shape[0] == 0:  # empty batch: nothing is launched, every gradient is zero
-            _zero_grads(grid_grads, flats)
-            pg = _split_param_grads(plan, flats, needs_params)
-            return (None, g_ro if need[1] else None, g_rd if need[2] else None, None, *grid_grads, *pg)
-        stream = torch.cuda.current_stream(device).cuda_stream
+            e.zero()
+            grid_grads, pg = e.outputs(needs_params)
+            _release(plan, e)
+            return (None, g_ro if need[1] else None, g_rd if need[2] else None, None, *grid_grads,
+                    *NiceRenderFn._param_outputs(ctx, pg))
         defer = ctx.defer if any(needs_params) else None
         if defer is not None:
             a.flags |= L.NC_DEFER_PARAM_GRADS
@@ -535,12 +655,23 @@ class NiceRenderFn(torch.autograd.Function):
                     "nc_render_backward")
         finally:
             a.flags &= ~L.NC_DEFER_PARAM_GRADS
-        pg = _split_param_grads(plan, flats, needs_params)
+        grid_grads, pg = e.outputs(needs_params)
         if defer is not None:  # weight gradients: launched and attached by defer.run()
-            defer._add(L.NcRenderArgs.from_buffer_copy(a), ctx.ws, ctx.nbytes, flats,
+            defer._add(L.NcRenderArgs.from_buffer_copy(a), ctx.ws, ctx.nbytes, e.flats,
                        [(p, g) for p, g in zip(ctx.keep[5], pg) if g is not None])
             pg = [None] * len(pg)
-        return (None, g_ro if need[1] else None, g_rd if need[2] else None, None, *grid_grads, *pg)
+        _release(plan, e)
+        return (None, g_ro if need[1] else None, g_rd if need[2] else None, None, *grid_grads,
+                *NiceRenderFn._param_outputs(ctx, pg))
+
+    @staticmethod
+    def _param_outputs(ctx, pg):
+        """The gradients returned for the parameter inputs: the parameters' own, or in
+        the direct mode None for the anchor after attaching them to .grad here."""
+        if not ctx.direct:
+            return pg
+        _attach([(p, g) for p, g in zip(ctx.keep[5], pg) if g is not None])
+        return [None] * ctx.n_param_inputs
 
 
 class DeferParamGrads:
@@ -567,7 +698,7 @@ class DeferParamGrads:
     def run(self):
         lib = L.load()
         for args, ws, nbytes, _flats, pairs in self.pending:
-            stream = torch.cuda.current_stream(ws.device).cuda_stream
+            stream = _stream(ws.device)
             L.check(lib.nc_render_backward_params(ctypes.byref(args), ws.data_ptr(), nbytes, stream),
                     "nc_render_backward_params")
             for p, g in pairs:
@@ -599,16 +730,15 @@ class NiceEvalFn(torch.autograd.Function):
         for k in plan.grids:
             if grids[k] is None:
                 raise L.NiceCoreError(f"stage needs {L.GRID_KEYS[k]}")
-            g = grids[k].detach()
-            _fill_grid(a.grids[k], g, device)
-            gkeep.append(g)
+            _fill_grid_cached(a.grids[k], grids[k], device)
+            gkeep.append(grids[k].detach())
         if a.flags & L.NC_SAVE_FOR_BACKWARD:
             _bind_sparse(sparse, a, plan, P)
         raw = torch.empty(P, 4, device=device, dtype=torch.float32)
         a.raw = raw.data_ptr()
         nbytes = lib.nc_points_workspace_bytes(ctypes.byref(a))
         ws = torch.empty(max(nbytes, 1), device=device, dtype=torch.uint8)
-        stream = torch.cuda.current_stream(device).cuda_stream
+        stream = _stream(device)
         L.check(lib.nc_points_forward(ctypes.byref(a), ws.data_ptr(), nbytes, stream), "nc_points_forward")
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
         ctx.sparse = sparse
@@ -629,15 +759,18 @@ class NiceEvalFn(torch.autograd.Function):
         g_pts = torch.empty_like(pts) if need[1] else None
         a.g_pts = _ptr(g_pts)
         needs_params = need[6:]
-        grid_grads, flats = _alloc_grads(lib, plan, needs_params, _dense_needs(need[2:6], ctx.sparse), ctx.grids,
-                                         a, device, sparse=ctx.sparse)
-        stream = torch.cuda.current_stream(device).cuda_stream
+        stream = _stream(device)
+        e, _ = _grad_buffer(lib, plan, needs_params, _dense_needs(need[2:6], ctx.sparse), ctx.grids, device, stream)
+        if e.gsize:
+            e.buf[:e.gsize].zero_()
+        e.bind(a, plan, ctx.sparse)
         if a.n_points == 0:  # no points: nothing is launched, every gradient is zero
-            _zero_grads(grid_grads, flats)
+            e.zero()
         else:
             L.check(lib.nc_points_backward(ctypes.byref(a), ctx.ws.data_ptr(), ctx.nbytes, stream),
                     "nc_points_backward")
-        pg = _split_param_grads(plan, flats, needs_params)
+        grid_grads, pg = e.outputs(needs_params)
+        _release(plan, e)
         gp = g_pts.to(ctx.p_dtype).reshape(ctx.p_shape) if g_pts is not None else None
         return (None, gp, *grid_grads, *pg)
 

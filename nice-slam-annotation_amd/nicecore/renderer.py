@@ -41,6 +41,9 @@ class Renderer(object):
         self.N_samples = r['N_samples']
         self.N_surface = r['N_surface']
         self.N_importance = r['N_importance']
+        # extension: how the decoder parameters get their .grad ("autograd" | "direct",
+        # render_fn.param_inputs); absent from the reference configs = the default
+        self.param_grads = r.get('param_grads')
         self.scale = cfg['scale']
         self.occupancy = cfg['occupancy']
         self.nice = slam.nice
@@ -97,7 +100,7 @@ class Renderer(object):
         return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
                            self.N_samples, self.N_surface, depth_max, sparse_grads=sparse_grads,
                            n_importance=self.N_importance, perturb=self.perturb, lindisp=self.lindisp,
-                           t_rand=t_rand)
+                           t_rand=t_rand, param_grads=self.param_grads)
 
     def render_batch_loss(self, c, decoders, rays_d, rays_o, device, stage, gt_depth, gt_color=None,
                           loss='mapper', w_color_loss=0.2, color_term=False, handle_dynamic=False,
@@ -116,7 +119,7 @@ class Renderer(object):
                                 render_gt_depth, self.N_samples, self.N_surface, depth_max,
                                 sparse_grads=sparse_grads, n_importance=self.N_importance,
                                 perturb=self.perturb, defer_param_grads=defer_param_grads,
-                                lindisp=self.lindisp, t_rand=t_rand)
+                                lindisp=self.lindisp, t_rand=t_rand, param_grads=self.param_grads)
 
     def regulation(self, c, decoders, rays_d, rays_o, gt_depth, device, stage='color', t_rand=None):
         """Renderer.py:343-409 (iMAP* only): densities of N_samples points per ray in

@@ -112,7 +112,7 @@ class SampleRaysFn(torch.autograd.Function):
             a.bound = b.data_ptr()
             inside = torch.empty(F * n, device=device, dtype=torch.bool)
             a.inside = inside.data_ptr()
-        stream = torch.cuda.current_stream(device).cuda_stream
+        stream = L.raw_stream(device)
         L.check(lib.nc_sample_rays_forward(ctypes.byref(a), stream), "nc_sample_rays_forward")
         ctx.args, ctx.keep = a, keep
         ctx.c2w_shape = c2w_d.shape
@@ -132,7 +132,7 @@ class SampleRaysFn(torch.autograd.Function):
         a.g_rays_d = gd.data_ptr() if gd is not None else None
         g34 = torch.empty(c2w.shape[0], 3, 4, device=c2w.device, dtype=c2w.dtype)
         a.g_c2w = g34.data_ptr()
-        stream = torch.cuda.current_stream(c2w.device).cuda_stream
+        stream = L.raw_stream(c2w.device)
         L.check(lib.nc_sample_rays_backward(ctypes.byref(a), stream), "nc_sample_rays_backward")
         if ctx.c2w_shape[1] == 3:
             g = g34

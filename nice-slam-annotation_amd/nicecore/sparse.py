@@ -123,7 +123,7 @@ class SparseGridGrads:
         """Forget every claimed row (nc_sparse_rows_clear: map entries back to -1)."""
         lib = L.load()
         for r in self.rows.values():
-            stream = torch.cuda.current_stream(r.device).cuda_stream
+            stream = L.raw_stream(r.device)
             st = r.struct()
             L.check(lib.nc_sparse_rows_clear(ctypes.byref(st), stream), "nc_sparse_rows_clear")
             r.claim_bound = 0
@@ -198,7 +198,7 @@ class SparseGridGrads:
         host = dist.get_backend(group) == "gloo"
         lib = L.load()
         for key, r in self.rows.items():
-            stream = torch.cuda.current_stream(r.device).cuda_stream
+            stream = L.raw_stream(r.device)
             # every rank contributes a fixed-size block: the largest capacity of any rank
             cap = torch.tensor([r.capacity], dtype=torch.int64, device="cpu" if host else r.device)
             dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=group)

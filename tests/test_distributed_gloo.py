@@ -176,6 +176,30 @@ def test_shared_buffer_ranges():
     assert sorted(r.numel() for r in ranges) == [8, 16] and len(rest) == 1
 
 
+def test_shared_buffer_after_accumulate_grad():
+    """The grads AccumulateGrad stores (detached aliases, no ._base) of views of one
+    buffer are still found to share it: grouped by storage, one range."""
+    from nicecore import distributed as ND
+    buf = torch.zeros(20)
+
+    class Fn(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, a, b, c):
+            return a.sum() + b.sum() + c.sum()
+
+        @staticmethod
+        def backward(ctx, g):
+            return (torch.as_strided(buf, (1, 2, 2, 1, 2), (8, 1, 4, 2, 2), 0), buf[8:14].view(2, 3),
+                    buf[14:20].detach())
+    a = torch.zeros(1, 2, 2, 1, 2).contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+    b = torch.zeros(2, 3, requires_grad=True)
+    c = torch.zeros(6, requires_grad=True)
+    Fn.apply(a, b, c).backward()
+    assert a.grad._base is None and a.grad.data_ptr() == buf.data_ptr()
+    ranges, rest = ND._shared_bases([a.grad, b.grad, c.grad])
+    assert rest == [] and [r.numel() for r in ranges] == [20] and ranges[0].data_ptr() == buf.data_ptr()
+
+
 def _rows_worker(rank, world, port, out):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
