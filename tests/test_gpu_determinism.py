@@ -118,8 +118,8 @@ def test_frustum_masked_nonleaf_grids(deterministic):
 @pytest.mark.gpu
 def test_deterministic_graph_replay_bitwise(monkeypatch):
     """NC_DETERMINISTIC inside a replayed hipGraph at the bench size (1000 rays x 48
-    samples x 3 decoders = 1.15M sorted entries, past rocprim's 1M-item switch to its
-    look-back sort, which hung in graph replays: nc_det.hip keeps the merge path): 40
+    samples x 3 decoders = 1.15M sorted entries; rocprim's look-back sort hung in graph
+    replays at this size, nc_det.hip sorts with its own capture-safe radix passes): 40
     replays, every one bit-identical to the eager deterministic gradients."""
     from nicecore.graph import GraphedStep
     monkeypatch.setenv("NC_DETERMINISTIC", "1")
