@@ -1024,7 +1024,7 @@ struct ImapOff {
 
 struct ImapWs {
   size_t dmax = 0, z = 0, pts = 0, pf = 0, emb = 0, h = 0, raw = 0, occ = 0, rgb = 0;
-  size_t gocc = 0, grgb = 0, dout = 0, dz = 0, demb = 0, dx = 0, dpts = 0, gnorm = 0, total = 0;
+  size_t gocc = 0, grgb = 0, dout = 0, dz = 0, demb = 0, dx = 0, dpts = 0, gnorm = 0, wt = 0, total = 0;
 };
 
 void imap_layout(int64_t N, int64_t P, bool rays, bool bwd, ImapWs& w) {
@@ -1054,6 +1054,7 @@ void imap_layout(int64_t N, int64_t P, bool rays, bool bwd, ImapWs& w) {
     take(w.demb, (size_t)P * EMBP * 4);
     take(w.dx, (size_t)P * EMBP * 4);
     take(w.dpts, (size_t)P * 24);
+    take(w.wt, (size_t)(3 * IH + EMB) * IH * 4);  // W_1..3^T, W_0^T: the dX GEMMs' k-contiguous B
   }
   w.total = o;
 }
@@ -1102,9 +1103,9 @@ int imap_mlp_forward(const nc_imap_params& d, int64_t P, void* ws, const ImapWs&
     g.relu = 1;
     if (int e = run_gemm(g, false, false, s)) return e;
   }
-  ImapGemm g = gemm(h + 3 * P * IH, IH, d.out_w, IH, raw, 4, P, 4, IH);
-  g.bias = d.out_b;
-  return run_gemm(g, false, false, s);
+  // output layer (N = 4): a streaming kernel, not a 64-wide MFMA tile
+  return check_hip(timed(KID_IMAP_GEMM, s, [&] { return launch_imap_out(h + 3 * P * IH, d.out_w, d.out_b, P, raw, s); }),
+                   "k_imap_out");
 }
 
 // backward from d raw [P][4] (dout): ReLU-masked dX chain, Fourier backward, and the
@@ -1118,21 +1119,34 @@ int imap_mlp_backward(const nc_imap_params& d, int64_t P, void* ws, const ImapWs
   float* demb = at<float>(ws, w.demb);
   float* dx = d.grad ? at<float>(ws, w.dx) : nullptr;
   const int64_t PH = P * IH;
-  {  // dz_3 = (dout W_out) . [h_3 > 0]
-    ImapGemm g = gemm(dout, 4, d.out_w, IH, dz + 3 * PH, IH, P, IH, 4);
-    g.mask = h + 3 * PH;
-    g.ldm = IH;
-    if (int e = run_gemm(g, false, true, s)) return e;
+  // W_l^T [in][out] (k = out contiguous): the dX GEMMs below read B(k, n) = W_l[k][n] as
+  // rows of W_l^T, the layout whose tiles load as float4 rows (k_imap_gemm_h)
+  float* wt = at<float>(ws, w.wt);
+  float* wtl[4] = {wt + 3 * (int64_t)IH * IH, wt, wt + (int64_t)IH * IH, wt + 2 * (int64_t)IH * IH};
+  {
+    ImapTranspose t;
+    std::memset(&t, 0, sizeof(t));
+    for (int l = 0; l < 4; ++l) {
+      t.src[l] = d.lin_w[l];
+      t.dst[l] = wtl[l];
+      t.rows[l] = IH;
+      t.cols[l] = l == 0 ? EMB : IH;
+    }
+    if (int e = check_hip(launch_imap_transpose(t, 4, s), "k_imap_transpose")) return e;
   }
+  // dz_3 = (dout W_out) . [h_3 > 0] (K = 4): a streaming kernel
+  if (int e = check_hip(timed(KID_IMAP_GEMM, s, [&] { return launch_imap_out_bwd(dout, d.out_w, h + 3 * PH, P, dz + 3 * PH, s); }),
+                        "k_imap_out_bwd"))
+    return e;
   for (int l = 3; l >= 1; --l) {  // dz_{l-1} = (dz_l W_l) . [h_{l-1} > 0]
-    ImapGemm g = gemm(dz + l * PH, IH, d.lin_w[l], IH, dz + (l - 1) * PH, IH, P, IH, IH);
+    ImapGemm g = gemm(dz + l * PH, IH, wtl[l], IH, dz + (l - 1) * PH, IH, P, IH, IH);
     g.mask = h + (l - 1) * PH;
     g.ldm = IH;
-    if (int e = run_gemm(g, false, true, s)) return e;
+    if (int e = run_gemm(g, false, false, s)) return e;
   }
   if (dpts || dx) {
-    ImapGemm g = gemm(dz, IH, d.lin_w[0], EMB, demb, EMBP, P, EMB, IH);  // d emb = dz_0 W_0
-    if (int e = run_gemm(g, false, true, s)) return e;
+    ImapGemm g = gemm(dz, IH, wtl[0], IH, demb, EMBP, P, EMB, IH);  // d emb = dz_0 W_0
+    if (int e = run_gemm(g, false, false, s)) return e;
     if (int e = check_hip(timed(KID_IMAP_FOURIER, s, [&] {
                             return launch_imap_fourier_bwd(pf, d.fourier_B, P, demb, dx, dpts, s);
                           }),

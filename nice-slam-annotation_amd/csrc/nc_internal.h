@@ -189,6 +189,14 @@ struct ImapGemm {
   int64_t k_split;     // set by the launcher
 };
 int launch_imap_gemm(const ImapGemm& g, bool a_kmajor, bool b_kn, hipStream_t s);
+struct ImapTranspose {  // dst[z] = src[z]^T, src[z] row-major [rows][cols]
+  const float* src[4];
+  float* dst[4];
+  int32_t rows[4], cols[4];
+};
+int launch_imap_transpose(const ImapTranspose& t, int n, hipStream_t s);
+int launch_imap_out(const float* h3, const float* wo, const float* bo, int64_t P, float* raw, hipStream_t s);
+int launch_imap_out_bwd(const float* dout, const float* wo, const float* h3, int64_t P, float* dz3, hipStream_t s);
 int launch_imap_embed(const float4* pf, const float* B, int64_t P, float* emb, hipStream_t s);
 int launch_imap_fourier_bwd(const float4* pf, const float* B, int64_t P, const float* demb, float* dx, double* dpts,
                             hipStream_t s);

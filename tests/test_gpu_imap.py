@@ -271,3 +271,34 @@ def test_imap_refuses_deterministic_request(monkeypatch):
     for q in m.parameters():
         q.requires_grad_(False)
     assert m(p).shape == (64, 4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale", [4.0e4, 3.0e5])
+def test_imap_past_f16_range(scale):
+    """The layer GEMMs run on the split-f16 MFMA (nc_imap.hip k_imap_gemm_h); operands at
+    or past 2^15 make a workgroup recompute its tile on the exact f32 MFMA.  Block-0
+    weights scaled so every hidden activation is O(scale): outputs and gradients still
+    match the fp32 oracle (the reference's addmm) at the usual tolerances."""
+    bound, params = _scene()
+    params = {k: v.clone() for k, v in params.items()}
+    w = params["pts_linears.0.weight"]
+    params["pts_linears.0.weight"] = w / w.abs().max() * scale
+    P = 3000
+    g = torch.Generator().manual_seed(3)
+    p = (torch.rand(P, 3, generator=g, dtype=torch.float64) * 1.2 - 0.1)
+    m = _model(params)
+    pg = p.cuda().requires_grad_(True)
+    raw = m(pg)
+    up = torch.randn(P, 4, generator=g)
+    raw.backward(up.cuda())
+    prm = {k: v.float().clone().requires_grad_(True) for k, v in params.items()}
+    pc = p.clone().requires_grad_(True)
+    ref = IO.imap_forward(pc, prm)
+    ref.backward(up)
+    assert float(ref.abs().max()) > 1e3
+    assert bool(torch.isfinite(raw).all())
+    assert rel(raw, ref) <= OUT_TOL, rel(raw, ref)
+    assert rel(pg.grad, pc.grad) <= GRAD_TOL, rel(pg.grad, pc.grad)
+    for n, q in m.named_parameters():
+        assert rel(q.grad, prm[n].grad) <= GRAD_TOL, (n, rel(q.grad, prm[n].grad))

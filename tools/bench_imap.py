@@ -22,6 +22,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "nice-slam-annotation_amd")]
 
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, dense f32 MFMA
+SPLIT16_PEAK_TFLOPS = 2500.0 / 3  # dense f16 MFMA / 3 products per split-f16 product (k_imap_gemm_h)
 
 
 def main():
@@ -89,6 +90,9 @@ def main():
            "mfma_peak_tflops": F32_MFMA_PEAK_TFLOPS}
     if out["gemm_tflops"]:
         out["gemm_frac"] = round(out["gemm_tflops"] / F32_MFMA_PEAK_TFLOPS, 3)
+        out["gemm_kernel"] = "k_imap_gemm (f32 MFMA)" if os.environ.get("NC_IMAP_F32") == "1" else \
+            "k_imap_gemm_h (split-f16 MFMA; N < 64 layers on k_imap_gemm)"
+        out["gemm_frac_split16_peak"] = round(out["gemm_tflops"] / SPLIT16_PEAK_TFLOPS, 3)
     if args.cpu_rays:
         from oracle import imap_oracle as IO
         torch.set_num_threads(min(os.cpu_count() or 1, 16))
