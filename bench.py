@@ -198,7 +198,7 @@ def build_workload(args, rank, device, world=1):
     ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000 + rank)
     slam = types.SimpleNamespace(nice=True, bound=sc.bound, H=sc.H, W=sc.W, fx=sc.fx, fy=sc.fy,
                                  cx=sc.cx, cy=sc.cy)
-    cfg = {"rendering": dict(S.DEFAULT_RENDERING, param_grads=args.param_grads), "scale": 1, "occupancy": True}
+    cfg = {"rendering": dict(S.DEFAULT_RENDERING, param_grads=getattr(args, "param_grads", "autograd")), "scale": 1, "occupancy": True}
     renderer = Renderer(cfg, None, slam)
     ba = args.mode == "ba"
     for g in grids.values():
