@@ -1025,6 +1025,7 @@ struct ImapOff {
 struct ImapWs {
   size_t dmax = 0, z = 0, pts = 0, pf = 0, emb = 0, h = 0, raw = 0, occ = 0, rgb = 0;
   size_t gocc = 0, grgb = 0, dout = 0, dz = 0, demb = 0, dx = 0, dpts = 0, gnorm = 0, wt = 0, total = 0;
+  size_t wimg = 0, wflag = 0, wtimg = 0, wtflag = 0;  // split-f16 weight images (k_imap_wimage)
 };
 
 void imap_layout(int64_t N, int64_t P, bool rays, bool bwd, ImapWs& w) {
@@ -1038,6 +1039,8 @@ void imap_layout(int64_t N, int64_t P, bool rays, bool bwd, ImapWs& w) {
   take(w.pf, (size_t)P * 16);
   take(w.emb, (size_t)P * EMBP * 4);
   take(w.h, (size_t)4 * P * IH * 4);
+  take(w.wimg, (size_t)3 * IH * imap_wimage_row(IH));  // W_1..3 images, forward B
+  take(w.wflag, 16);
   take(w.raw, (size_t)P * 16);
   if (rays) {
     take(w.occ, (size_t)P * 4);
@@ -1055,6 +1058,8 @@ void imap_layout(int64_t N, int64_t P, bool rays, bool bwd, ImapWs& w) {
     take(w.dx, (size_t)P * EMBP * 4);
     take(w.dpts, (size_t)P * 24);
     take(w.wt, (size_t)(3 * IH + EMB) * IH * 4);  // W_1..3^T, W_0^T: the dX GEMMs' k-contiguous B
+    take(w.wtimg, (size_t)(3 * IH + EMB) * imap_wimage_row(IH));  // and their split-f16 images
+    take(w.wtflag, 16);
   }
   w.total = o;
 }
@@ -1095,12 +1100,34 @@ int imap_mlp_forward(const nc_imap_params& d, int64_t P, void* ws, const ImapWs&
   if (int e = check_hip(timed(KID_IMAP_FOURIER, s, [&] { return launch_imap_embed(pf, d.fourier_B, P, emb, s); }),
                         "k_imap_embed"))
     return e;
+  // W_1..3 split once per call (k_imap_gemm_h then copies their tiles)
+  unsigned char* wimg = at<unsigned char>(ws, w.wimg);
+  uint32_t* wflag = at<uint32_t>(ws, w.wflag);
+  const int64_t irow = imap_wimage_row(IH);
+  {
+    ImapWImage im;
+    std::memset(&im, 0, sizeof(im));
+    for (int z = 0; z < 3; ++z) {
+      im.src[z] = d.lin_w[z + 1];
+      im.img[z] = wimg + (int64_t)z * IH * irow;
+      im.N[z] = IH;
+      im.K[z] = IH;
+      im.ld[z] = IH;
+    }
+    im.flag = wflag;
+    if (int e = check_hip(launch_imap_wimage(im, 3, s), "k_imap_wimage")) return e;
+  }
   for (int l = 0; l < 4; ++l) {
     const float* x = l == 0 ? emb : h + (int64_t)(l - 1) * P * IH;
     const int64_t K = l == 0 ? EMB : IH;
     ImapGemm g = gemm(x, l == 0 ? EMBP : IH, d.lin_w[l], K, h + (int64_t)l * P * IH, IH, P, IH, K);
     g.bias = d.lin_b[l];
     g.relu = 1;
+    if (l > 0) {
+      g.Bimg = wimg + (int64_t)(l - 1) * IH * irow;
+      g.bflag = wflag + (l - 1);
+      g.bimg_row = irow;
+    }
     if (int e = run_gemm(g, false, false, s)) return e;
   }
   // output layer (N = 4): a streaming kernel, not a 64-wide MFMA tile
@@ -1123,16 +1150,25 @@ int imap_mlp_backward(const nc_imap_params& d, int64_t P, void* ws, const ImapWs
   // rows of W_l^T, the layout whose tiles load as float4 rows (k_imap_gemm_h)
   float* wt = at<float>(ws, w.wt);
   float* wtl[4] = {wt + 3 * (int64_t)IH * IH, wt, wt + (int64_t)IH * IH, wt + 2 * (int64_t)IH * IH};
-  {
-    ImapTranspose t;
-    std::memset(&t, 0, sizeof(t));
+  unsigned char* wtimg = at<unsigned char>(ws, w.wtimg);
+  uint32_t* wtflag = at<uint32_t>(ws, w.wtflag);
+  const int64_t irow = imap_wimage_row(IH);
+  unsigned char* timg[4] = {wtimg + 3 * (int64_t)IH * irow, wtimg, wtimg + (int64_t)IH * irow,
+                            wtimg + 2 * (int64_t)IH * irow};
+  {  // W_l^T as f32 (the exact fallback's B) and as split-f16 images, one launch
+    ImapWImage im;
+    std::memset(&im, 0, sizeof(im));
     for (int l = 0; l < 4; ++l) {
-      t.src[l] = d.lin_w[l];
-      t.dst[l] = wtl[l];
-      t.rows[l] = IH;
-      t.cols[l] = l == 0 ? EMB : IH;
+      im.src[l] = d.lin_w[l];
+      im.img[l] = timg[l];
+      im.f32t[l] = wtl[l];
+      im.N[l] = l == 0 ? EMB : IH;  // rows of W_l^T = inputs of layer l
+      im.K[l] = IH;
+      im.ld[l] = l == 0 ? EMB : IH;
+      im.trans[l] = 1;
     }
-    if (int e = check_hip(launch_imap_transpose(t, 4, s), "k_imap_transpose")) return e;
+    im.flag = wtflag;
+    if (int e = check_hip(launch_imap_wimage(im, 4, s), "k_imap_wimage")) return e;
   }
   // dz_3 = (dout W_out) . [h_3 > 0] (K = 4): a streaming kernel
   if (int e = check_hip(timed(KID_IMAP_GEMM, s, [&] { return launch_imap_out_bwd(dout, d.out_w, h + 3 * PH, P, dz + 3 * PH, s); }),
@@ -1142,10 +1178,16 @@ int imap_mlp_backward(const nc_imap_params& d, int64_t P, void* ws, const ImapWs
     ImapGemm g = gemm(dz + l * PH, IH, wtl[l], IH, dz + (l - 1) * PH, IH, P, IH, IH);
     g.mask = h + (l - 1) * PH;
     g.ldm = IH;
+    g.Bimg = timg[l];
+    g.bflag = wtflag + l;
+    g.bimg_row = irow;
     if (int e = run_gemm(g, false, false, s)) return e;
   }
   if (dpts || dx) {
     ImapGemm g = gemm(dz, IH, wtl[0], IH, demb, EMBP, P, EMB, IH);  // d emb = dz_0 W_0
+    g.Bimg = timg[0];
+    g.bflag = wtflag;
+    g.bimg_row = irow;
     if (int e = run_gemm(g, false, false, s)) return e;
     if (int e = check_hip(timed(KID_IMAP_FOURIER, s, [&] {
                             return launch_imap_fourier_bwd(pf, d.fourier_B, P, demb, dx, dpts, s);

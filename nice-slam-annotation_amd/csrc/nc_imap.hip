@@ -229,8 +229,27 @@ __device__ void h_exact_tile(const ImapGemm& g, int64_t m0, int64_t n0, int64_t 
   }
 }
 
-// B_VEC: B's rows are 16-B aligned (float4 loads); else scalar loads (W_0: 93 floats per row)
-template <bool B_VEC>
+// B's k-slice tile from its pre-split image (k_imap_wimage): 128 rows x 8 chunks of 16 B,
+// copied as they are (the image already holds the LDS tile's swizzled chunk order)
+__device__ __forceinline__ void h_img_load(const ImapGemm& g, int64_t n0, int64_t sl, uint4 (&v)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = threadIdx.x + 256 * j, row = e >> 3, c = e & 7;
+    const int64_t n = n0 + row;
+    v[j] = n < g.N ? *reinterpret_cast<const uint4*>(g.Bimg + n * g.bimg_row + sl * 128 + 16 * c) : uint4{0u, 0u, 0u, 0u};
+  }
+}
+__device__ __forceinline__ void h_img_stage(const uint4 (&v)[4], unsigned char* tile) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = threadIdx.x + 256 * j;
+    *reinterpret_cast<uint4*>(tile + (e >> 3) * HROW + 16 * (e & 7)) = v[j];
+  }
+}
+
+// B_VEC: B's rows are 16-B aligned (float4 loads); else scalar loads (W_0: 93 floats per row).
+// B_IMG: B staged from its pre-split image (no per-slice split of the weights)
+template <bool B_VEC, bool B_IMG>
 __global__ void __launch_bounds__(256, NC_IMAP_H_OCC) k_imap_gemm_h(const ImapGemm g, int mt, int nt) {
   constexpr bool A_KM = false, B_KN = false;
   extern __shared__ __attribute__((aligned(16))) unsigned char hl[];
@@ -249,14 +268,17 @@ __global__ void __launch_bounds__(256, NC_IMAP_H_OCC) k_imap_gemm_h(const ImapGe
   for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int v = 0; v < 4; ++v) acc[u][v] = accx[u][v] = zero4();
-  float amax = 0.f;
-  float xa[16], xb[16];
+  float amax = (B_IMG && *g.bflag) ? __builtin_inff() : 0.f;  // the image's own range flag
+  float xa[16], xb[B_IMG ? 1 : 16];
+  uint4 vb[B_IMG ? 4 : 1];
   const int64_t ns = (ke - kb + HK - 1) / HK;
   if (ns > 0) {
     h_load<A_KM>(g.A, g.lda, m0, g.M, kb, ke, xa);
-    h_load<B_KN, B_VEC>(g.B, g.ldb, n0, g.N, kb, ke, xb);
+    if constexpr (B_IMG) h_img_load(g, n0, kb / HK, vb);
+    else h_load<B_KN, B_VEC>(g.B, g.ldb, n0, g.N, kb, ke, xb);
     h_stage<A_KM>(xa, hl, amax);
-    h_stage<B_KN>(xb, hl + HT * HROW, amax);
+    if constexpr (B_IMG) h_img_stage(vb, hl + HT * HROW);
+    else h_stage<B_KN>(xb, hl + HT * HROW, amax);
   }
   __syncthreads();
   for (int64_t s = 0; s < ns; ++s) {
@@ -264,7 +286,8 @@ __global__ void __launch_bounds__(256, NC_IMAP_H_OCC) k_imap_gemm_h(const ImapGe
     if (more) {  // next slice's loads in flight during this slice's MFMAs
       const int64_t k1 = kb + (s + 1) * HK;
       h_load<A_KM>(g.A, g.lda, m0, g.M, k1, ke, xa);
-      h_load<B_KN, B_VEC>(g.B, g.ldb, n0, g.N, k1, ke, xb);
+      if constexpr (B_IMG) h_img_load(g, n0, k1 / HK, vb);
+      else h_load<B_KN, B_VEC>(g.B, g.ldb, n0, g.N, k1, ke, xb);
     }
     const unsigned char* As = hl + (s & 1) * H_STAGE;
     const unsigned char* Bs = As + HT * HROW;
@@ -290,7 +313,8 @@ __global__ void __launch_bounds__(256, NC_IMAP_H_OCC) k_imap_gemm_h(const ImapGe
     if (more) {
       unsigned char* nxt = hl + ((s + 1) & 1) * H_STAGE;
       h_stage<A_KM>(xa, nxt, amax);
-      h_stage<B_KN>(xb, nxt + HT * HROW, amax);
+      if constexpr (B_IMG) h_img_stage(vb, nxt + HT * HROW);
+      else h_stage<B_KN>(xb, nxt + HT * HROW, amax);
     }
     __syncthreads();
   }
@@ -320,28 +344,6 @@ __global__ void __launch_bounds__(256, NC_IMAP_H_OCC) k_imap_gemm_h(const ImapGe
         else g.C[m * g.ldc + n] = val;
       }
     }
-  }
-}
-
-// dst[c][r] = src[r][c] for up to 4 matrices (blockIdx.z): the transposed weights of
-// the backward's dX GEMMs (dz_{l-1} = dz_l W_l reads W_l^T rows, k contiguous), 32 x 32
-// tiles through LDS
-__global__ void __launch_bounds__(256) k_imap_transpose(const ImapTranspose t) {
-  __shared__ float tile[32][33];
-  const int z = blockIdx.z, R = t.rows[z], C = t.cols[z];
-  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
-  if (r0 >= R || c0 >= C) return;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-#pragma unroll
-  for (int k = 0; k < 32; k += 8) {
-    const int r = r0 + ty + k, c = c0 + tx;
-    tile[ty + k][tx] = (r < R && c < C) ? t.src[z][(int64_t)r * C + c] : 0.f;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 32; k += 8) {
-    const int c = c0 + ty + k, r = r0 + tx;
-    if (c < C && r < R) t.dst[z][(int64_t)c * R + r] = tile[tx][ty + k];
   }
 }
 
@@ -399,6 +401,36 @@ __global__ void __launch_bounds__(256) k_imap_out_bwd(const float* dout, const f
   }
   *reinterpret_cast<float4*>(dz3 + p * NC_IMAP_HIDDEN + n) =
       float4{m.x > 0.f ? v[0] : 0.f, m.y > 0.f ? v[1] : 0.f, m.z > 0.f ? v[2] : 0.f, m.w > 0.f ? v[3] : 0.f};
+}
+
+// Split-f16 images of the layer weights for k_imap_gemm_h's B operand: one thread per
+// (row n, k-slice, 8-value group g); the 8 values are split (split8) and written at the
+// chunk positions the LDS tile uses (hchunk of the tile row n & 127), so the GEMM copies
+// 16-B chunks without splitting.  Values at or past 2^15 set the matrix's flag (the GEMM
+// then takes its exact-f32 path).  trans: also the f32 B^T copy for that path.
+__global__ void __launch_bounds__(256) k_imap_wimage(const ImapWImage w) {
+  const int z = blockIdx.y;
+  const int N = w.N[z], K = w.K[z], ld = w.ld[z];
+  const int nsl = (K + 31) / 32;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)N * nsl * 4) return;
+  const int g = (int)(e & 3);
+  const int64_t rs = e >> 2;
+  const int n = (int)(rs / nsl), sl = (int)(rs - (int64_t)n * nsl);
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 32 * sl + 8 * g + j;
+    x[j] = k < K ? (w.trans[z] ? w.src[z][(int64_t)k * ld + n] : w.src[z][(int64_t)n * ld + k]) : 0.f;
+    if (w.trans[z] && w.f32t[z] && k < K) w.f32t[z][(int64_t)n * K + k] = x[j];
+  }
+  half8 hi, lo;
+  float amax = 0.f;
+  split8(x, hi, lo, amax);
+  unsigned char* row = w.img[z] + (int64_t)n * imap_wimage_row(K) + 128 * sl;
+  *reinterpret_cast<half8*>(row + hchunk(n & 127, g, 0)) = hi;
+  *reinterpret_cast<half8*>(row + hchunk(n & 127, g, 1)) = lo;
+  if (!(amax < RANGE_LIMIT)) w.flag[z] = 1u;
 }
 
 // emb[p][j] = sin(p.float() @ B)[j] for j < 93, 0 for the pad columns 93..95
@@ -504,7 +536,7 @@ static inline unsigned blocks_of(int64_t n, int b) { return (unsigned)((n + b - 
 
 // the split-f16 kernel takes the layer GEMMs whose operands are both k-contiguous
 // (forward: A = [P][K] activations, B = W [out][in]; dX: B = W^T, transposed once per
-// backward by k_imap_transpose), whose tiles it fills (M, N >= 64) and which have at
+// backward by k_imap_wimage), whose tiles it fills (M, N >= 64) and which have at
 // least one whole k-slice (K >= 32), with rows that take float4 loads.  The layer-0
 // forward (W_0: 93 floats per row) stays on k_imap_gemm: through the split kernel
 // (scalar B loads) its ReLU branches differed from the reference's on one element of
@@ -540,14 +572,15 @@ int launch_imap_gemm_h(const ImapGemm& g, bool a_km, bool b_kn, hipStream_t s) {
   if (splits < 1) splits = 1;
   const dim3 grid((unsigned)(((mt + 7) / 8) * 8 * nt), 1, (unsigned)splits);
   if (a_km || b_kn) return (int)hipErrorInvalidValue;  // k-strided operands: k_imap_gemm
-  hipLaunchKernelGGL((k_imap_gemm_h<true>), grid, dim3(256), H_LDS, s, c, mt, nt);
+  if (c.Bimg) hipLaunchKernelGGL((k_imap_gemm_h<true, true>), grid, dim3(256), H_LDS, s, c, mt, nt);
+  else hipLaunchKernelGGL((k_imap_gemm_h<true, false>), grid, dim3(256), H_LDS, s, c, mt, nt);
   return (int)hipGetLastError();
 }
 
 int launch_imap_gemm(const ImapGemm& g, bool a_km, bool b_kn, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return 0;
   if (!imap_f32_forced() && !a_km && !b_kn && g.M >= 64 && g.N >= 64 && g.K >= HK && h_vec_ok(g.A, g.lda, false) &&
-      h_vec_ok(g.B, g.ldb, false))
+      (g.Bimg || h_vec_ok(g.B, g.ldb, false)))
     return launch_imap_gemm_h(g, a_km, b_kn, s);
   ImapGemm c = g;
   int splits = 1;
@@ -571,17 +604,6 @@ int launch_imap_gemm(const ImapGemm& g, bool a_km, bool b_kn, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int launch_imap_transpose(const ImapTranspose& t, int n, hipStream_t s) {
-  int R = 0, C = 0;
-  for (int z = 0; z < n; ++z) {
-    R = t.rows[z] > R ? t.rows[z] : R;
-    C = t.cols[z] > C ? t.cols[z] : C;
-  }
-  if (n <= 0 || R <= 0 || C <= 0) return 0;
-  hipLaunchKernelGGL(k_imap_transpose, dim3(blocks_of(C, 32), blocks_of(R, 32), (unsigned)n), dim3(256), 0, s, t);
-  return (int)hipGetLastError();
-}
-
 int launch_imap_out(const float* h3, const float* wo, const float* bo, int64_t P, float* raw, hipStream_t s) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(k_imap_out, dim3(blocks_of(P, 64)), dim3(256), 0, s, h3, wo, bo, P, raw);
@@ -592,6 +614,18 @@ int launch_imap_out_bwd(const float* dout, const float* wo, const float* h3, int
   if (P <= 0) return 0;
   hipLaunchKernelGGL(k_imap_out_bwd, dim3(blocks_of(P * (NC_IMAP_HIDDEN / 4), 256)), dim3(256), 0, s, dout, wo, h3, P,
                      dz3);
+  return (int)hipGetLastError();
+}
+
+int launch_imap_wimage(const ImapWImage& w, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (int e = (int)hipMemsetAsync(w.flag, 0, 4 * sizeof(uint32_t), s)) return e;
+  int64_t most = 0;
+  for (int z = 0; z < n; ++z) {
+    const int64_t c = (int64_t)w.N[z] * ((w.K[z] + 31) / 32) * 4;
+    most = c > most ? c : most;
+  }
+  hipLaunchKernelGGL(k_imap_wimage, dim3(blocks_of(most, 256), (unsigned)n), dim3(256), 0, s, w);
   return (int)hipGetLastError();
 }
 

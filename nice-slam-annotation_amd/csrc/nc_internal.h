@@ -187,14 +187,22 @@ struct ImapGemm {
   int32_t relu;
   int32_t atomic;      // accumulate with float atomics (split over K)
   int64_t k_split;     // set by the launcher
+  // optional pre-split image of B (k_imap_wimage): row n = ceil(K/32) slices of 128 B
+  // (hi | lo f16, k_mlp_fwd's swizzled chunk layout); bflag != 0: B reached 2^15
+  const unsigned char* Bimg;
+  const uint32_t* bflag;
+  int64_t bimg_row;    // bytes per image row
 };
 int launch_imap_gemm(const ImapGemm& g, bool a_kmajor, bool b_kn, hipStream_t s);
-struct ImapTranspose {  // dst[z] = src[z]^T, src[z] row-major [rows][cols]
+struct ImapWImage {  // split-f16 images of up to 4 matrices, B(k, n) = trans ? src[k*ld+n] : src[n*ld+k]
   const float* src[4];
-  float* dst[4];
-  int32_t rows[4], cols[4];
+  unsigned char* img[4];   // [N][ceil(K/32)][128 B]
+  float* f32t[4];          // optional: B^T as f32 [N][K] (trans only; the exact fallback's copy)
+  int32_t N[4], K[4], ld[4], trans[4];
+  uint32_t* flag;          // [4], zeroed by the launcher
 };
-int launch_imap_transpose(const ImapTranspose& t, int n, hipStream_t s);
+int launch_imap_wimage(const ImapWImage& w, int n, hipStream_t s);
+__host__ __device__ inline int64_t imap_wimage_row(int64_t K) { return (K + 31) / 32 * 128; }
 int launch_imap_out(const float* h3, const float* wo, const float* bo, int64_t P, float* raw, hipStream_t s);
 int launch_imap_out_bwd(const float* dout, const float* wo, const float* h3, int64_t P, float* dz3, hipStream_t s);
 int launch_imap_embed(const float4* pf, const float* B, int64_t P, float* emb, hipStream_t s);

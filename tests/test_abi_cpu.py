@@ -34,6 +34,12 @@ def test_every_declared_symbol_is_exported(lib):
         assert hasattr(lib, name), name
 
 
+def test_library_binds_every_symbol_now():
+    """dlopen with RTLD_NOW: an internal function left undefined (a launcher removed while
+    a caller remains) fails here instead of at its first call on the GPU."""
+    ctypes.CDLL(B.LIB, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+
+
 def test_struct_layouts_match(lib):
     assert lib.nc_struct_size(0) == ctypes.sizeof(L.NcRenderArgs)
     assert lib.nc_struct_size(1) == ctypes.sizeof(L.NcPointsArgs)
