@@ -91,10 +91,10 @@ def parse():
                     help="render with the loss target as gt_depth (Mapper / Tracker, S = 48) or "
                          "without one (S = 32: BASELINE configs[0], the reference's CPU plumbing "
                          "case C1; the loss still compares with the targets)")
-    ap.add_argument("--param-grads", default="autograd", choices=["autograd", "direct"],
+    ap.add_argument("--param-grads", default="direct", choices=["autograd", "direct"],
                     help="how the decoder parameters get .grad in the drop-in step (render_fn.param_inputs): "
-                         "through autograd (default, what the unmodified Mapper/Tracker run) or written by the "
-                         "backward itself (opt-in rendering.param_grads: direct); both eager times are reported")
+                         "written by the backward itself (the library default) or through autograd's "
+                         "AccumulateGrad (rendering.param_grads: autograd); both eager times are reported")
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
@@ -198,7 +198,7 @@ def build_workload(args, rank, device, world=1):
     ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000 + rank)
     slam = types.SimpleNamespace(nice=True, bound=sc.bound, H=sc.H, W=sc.W, fx=sc.fx, fy=sc.fy,
                                  cx=sc.cx, cy=sc.cy)
-    cfg = {"rendering": dict(S.DEFAULT_RENDERING, param_grads=getattr(args, "param_grads", "autograd")), "scale": 1, "occupancy": True}
+    cfg = {"rendering": dict(S.DEFAULT_RENDERING, param_grads=getattr(args, "param_grads", "direct")), "scale": 1, "occupancy": True}
     renderer = Renderer(cfg, None, slam)
     ba = args.mode == "ba"
     for g in grids.values():

@@ -80,7 +80,7 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     pass, ``sample_pdf`` (deterministic u when ``perturb`` == 0, as the reference), and
     the differentiable render over the sorted union of both sample sets.
 
-    ``param_grads``: "autograd" (default) or "direct" -- how the decoder parameters get
+    ``param_grads``: "direct" (default) or "autograd" -- how the decoder parameters get
     their ``.grad`` (render_fn.param_inputs)."""
     if stage == 'coarse':
         gt_depth = None

@@ -451,7 +451,7 @@ def _release(plan, entry):
 
 PARAM_GRAD_MODES = ("autograd", "direct")
 # default for render_rays / render_rays_loss / Renderer when the caller does not choose
-_PARAM_GRADS = os.environ.get("NICECORE_PARAM_GRADS", "autograd")
+_PARAM_GRADS = os.environ.get("NICECORE_PARAM_GRADS", "direct")
 _requires_grad = operator.attrgetter("requires_grad")
 _ANCHORS = {}  # device -> zero-size leaf that connects a "direct" render to the graph
 
@@ -459,17 +459,19 @@ _ANCHORS = {}  # device -> zero-size leaf that connects a "direct" render to the
 def param_inputs(spec, plan, device, mode=None):
     """The decoder-parameter inputs of NiceRenderFn.
 
-    ``"autograd"`` (default): the parameters themselves, so their gradients reach
-    ``.grad`` through AccumulateGrad like any autograd leaf (hooks, autograd.grad,
-    DDP all see them).
-    ``"direct"`` (opt-in: ``rendering: {param_grads: direct}`` in the config, or
-    ``NICECORE_PARAM_GRADS=direct``): the parameters stay out of the autograd graph
-    and the backward writes their ``.grad`` itself -- set when None, added otherwise,
-    the values AccumulateGrad would give.  One zero-size anchor leaf stands in for
-    them, so ~80 AccumulateGrad nodes and Function inputs per call disappear from the
-    host path (the Mapper's loss.backward(); optimizer.step() loop, Mapper.py:598-625,
-    sees the same .grad).  Not for callers that hook the decoder parameters or take
-    their gradients with torch.autograd.grad."""
+    ``"direct"`` (default): the parameters stay out of the autograd graph and the
+    backward writes their ``.grad`` itself -- set when None, added otherwise, the values
+    AccumulateGrad would give (also when other terms of the loss reach the same
+    parameters through autograd: whichever runs second adds).  One zero-size anchor
+    leaf stands in for them, so ~80 AccumulateGrad nodes and Function inputs per call
+    disappear from the host path; the reference's loops (loss.backward();
+    optimizer.step(); optimizer.zero_grad(), Mapper.py:598-625, Tracker.py:113-135) see
+    the same .grad.  What it does not support: hooks on the decoder parameters,
+    torch.autograd.grad / backward(inputs=...) restricted to them.
+    ``"autograd"`` (``rendering: {param_grads: autograd}`` in the config, or
+    ``NICECORE_PARAM_GRADS=autograd``): the parameters themselves, so their gradients
+    reach ``.grad`` through AccumulateGrad like any autograd leaf (hooks,
+    autograd.grad and DDP see them), at ~0.3 ms more host time per call at C2."""
     mode = mode or _PARAM_GRADS
     if mode == "autograd":
         return plan._flat

@@ -1,6 +1,7 @@
-"""Host logic of the decoder-parameter gradient modes (render_fn.param_inputs): the
-default hands the parameters to autograd; "direct" replaces them with one zero-size
-anchor leaf and records which of them need a gradient; unknown modes are refused."""
+"""Host logic of the decoder-parameter gradient modes (render_fn.param_inputs):
+"autograd" hands the parameters to autograd; "direct" (the default) replaces them with
+one zero-size anchor leaf and records which of them need a gradient; unknown modes are
+refused."""
 import pytest
 import torch
 
@@ -36,6 +37,14 @@ def test_direct_mode_anchor_and_needs():
         spec = {}
         assert param_inputs(spec, plan, torch.device("cpu"), "direct") == ()
         assert not any(spec["param_needs"])
+
+
+def test_default_mode_is_direct(monkeypatch):
+    from nicecore import render_fn as RF
+    model, plan = _plan()
+    spec = {}
+    ins = RF.param_inputs(spec, plan, torch.device("cpu"))
+    assert RF._PARAM_GRADS == "direct" and len(ins) == 1 and "param_needs" in spec
 
 
 def test_unknown_mode_refused():
