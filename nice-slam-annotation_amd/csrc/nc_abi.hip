@@ -9,6 +9,7 @@
 // device allocation (graph-capturable).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -38,14 +39,14 @@ enum KernelId {
   KID_PARAM_REDUCE, KID_RAY_GRADS, KID_POINTS_ASSEMBLE, KID_POINTS_SPLIT, KID_POINTS_GRADS, KID_GRID_BWD, KID_MLP_DW,
   KID_GRID_GATHER, KID_LOSS, KID_DET_SCATTER, KID_SAMPLE_RAYS, KID_SAMPLE_POSE_GRAD, KID_FRUSTUM, KID_ROWS_CLEAR,
   KID_ROWS_MERGE, KID_ROWS_CLAIM, KID_PARAM_RAY, KID_SAMPLE_PDF, KID_ADAM, KID_IMAP_GEMM, KID_IMAP_FOURIER, KID_GRID_ROWS,
-  KID_COUNT
+  KID_COMPOSITE_FWD_LOSS, KID_COUNT
 };
 const char* kKernelNames[KID_COUNT] = {"k_depth_max", "k_ray_setup", "k_mlp_fwd", "k_composite_fwd",
                                        "k_composite_bwd", "k_mlp_dx", "k_param_reduce", "k_ray_grads",
                                        "k_points_assemble", "k_points_split_grad", "k_points_grads", "k_grid_bwd",
                                        "k_mlp_dw", "k_grid_gather", "k_loss", "k_det_scatter",
                                        "k_sample_rays", "k_sample_pose_grad", "k_frustum_mask", "k_rows_clear", "k_rows_merge", "k_rows_compact", "k_param_ray_reduce", "k_sample_pdf", "k_adam",
-                                       "k_imap_gemm", "k_imap_fourier", "k_grid_rows"};
+                                       "k_imap_gemm", "k_imap_fourier", "k_grid_rows", "k_composite_fwd_loss"};
 struct TimedLaunch {
   hipEvent_t b, e;
   int id;
@@ -436,6 +437,18 @@ int gather_and_claim(MlpCtx& m, const Ws& w, hipStream_t s) {
   return 0;
 }
 
+// NC_LOSS_MAPPER forward for a backward: compositing, loss terms and the compositing
+// backward for d loss = 1 in one kernel (k_composite_fwd_loss; NICECORE_FUSED_LOSS=0 for
+// the three-kernel path).  NC_DETERMINISTIC keeps k_loss's fixed-order loss sum.
+bool fused_mapper_loss(const nc_render_args* a) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = std::getenv("NICECORE_FUSED_LOSS");
+    on = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+  }
+  return on && a->loss == NC_LOSS_MAPPER && (a->flags & NC_SAVE_FOR_BACKWARD) && !(a->flags & NC_DETERMINISTIC);
+}
+
 int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S) {
   if (!a) return fail(-1, "nicecore: args is NULL");
   if (a->abi_version != NC_ABI_VERSION) return fail(-2, "nicecore: ABI version mismatch");
@@ -688,6 +701,7 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     return fail(-1, "nicecore: NULL ray input or output pointer");
   RayCtx rc;
   fill_ray(rc, a, pl, ws, w, P, S);
+  rc.fuse_bwd = fused_mapper_loss(a);
   if (a->gt_depth && !a->depth_max) {
     if (a->n_rays <= kDmaxLocalRays) {
       rc.dmax_local = 1;  // reduced inside k_ray_setup
@@ -716,6 +730,9 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     m.zero_n4 = 0;
   }
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
+  if (rc.fuse_bwd)
+    return check_hip(timed(KID_COMPOSITE_FWD_LOSS, s, [&] { return launch_composite_fwd_loss(rc, s); }),
+                     "k_composite_fwd_loss");
   if (int e = check_hip(timed(KID_COMPOSITE_FWD, s, [&] { return launch_composite_fwd(rc, s); }), "k_composite_fwd")) return e;
   if (a->loss != NC_LOSS_NONE)
     if (int e = check_hip(timed(KID_LOSS, s, [&] { return launch_loss(rc, s); }), "k_loss")) return e;
@@ -743,7 +760,12 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   bool any = need_coord;
   for (int j = 0; j < m.n_jobs; ++j) any |= m.jobs[j].need_dw || m.jobs[j].need_grid;
   if (!any) return 0;
-  if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd")) return e;
+  // a fused mapper loss whose only upstream gradient is d loss: the forward's
+  // k_composite_fwd_loss already wrote d raw for d loss = 1, k_mlp_dx scales by d loss
+  if (fused_mapper_loss(a) && a->g_loss && !a->g_depth && !a->g_var && !a->g_color)
+    m.dout_scale = a->g_loss;
+  else if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd"))
+    return e;
   const DetBufs det = det_bufs(ws, w);
   return mlp_backward(m, a->dec, P, s, &det, need_coord ? &rc : nullptr,  // (+ ray grads, fused)
                       (a->flags & NC_DEFER_PARAM_GRADS) != 0);

@@ -71,6 +71,8 @@ struct MlpCtx {
                              // (k_mlp_dx stores them instead of scattering with atomics), else NULL
   float* bslab;              // [n_jobs][bslab_rows][DX_BSLAB] Fourier-B gradient partials, one row per
   int32_t bslab_rows;        // k_mlp_dx workgroup (= its grid x); k_mlp_dw moves them into its slab
+  const double* dout_scale;  // device scalar multiplying gocc / grgb in k_mlp_dx (d loss of a fused
+                             // mapper loss, RayCtx::fuse_bwd), or NULL
   uint32_t* range_flag;      // [MAX_JOBS] split-f16 range guard: k_mlp_fwd sets job j's word when
                              // an operand reached RANGE_LIMIT, k_mlp_fwd_exact then recomputes the
                              // job in f32; zeroed by k_ray_setup / k_points_prep (NULL: no guard)
@@ -172,6 +174,8 @@ struct RayCtx {
   // k_ray_grads adds gnorm * rays_d / ||rays_d|| to g_rays_d
   int32_t density;
   float* gnorm;              // [N]
+  int32_t fuse_bwd;          // NC_LOSS_MAPPER forward for a backward: k_composite_fwd_loss writes the
+                             // loss's d raw for d loss = 1 (gocc / grgb); no k_loss, no k_composite_bwd
 };
 
 // One layer GEMM of the iMAP* MLP (nc_imap.hip): C[m][n] (+)= sum_k A(m,k) B(k,n)
@@ -229,6 +233,7 @@ constexpr int DX_BSLAB = 3 * 96;  // floats per k_mlp_dx workgroup: d B [3][EMBP
 int launch_depth_max(const float* gt, int64_t n, float* out, hipStream_t s);
 int launch_ray_setup(const RayCtx& c, hipStream_t s);
 int launch_composite_fwd(const RayCtx& c, hipStream_t s);
+int launch_composite_fwd_loss(const RayCtx& c, hipStream_t s);
 int launch_composite_bwd(const RayCtx& c, hipStream_t s);
 int launch_ray_grads(const RayCtx& c, hipStream_t s);
 int launch_loss(const RayCtx& c, hipStream_t s);

@@ -860,6 +860,7 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
   load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
   float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
   const int64_t ntiles = (ctx.P + 15) / 16;
+  const float dscale = ctx.dout_scale ? (float)*ctx.dout_scale : 1.f;  // fused mapper loss: d loss
   for (int64_t t = (int64_t)blockIdx.x * waves + wave; t < ntiles; t += (int64_t)gridDim.x * waves) {
     asm volatile("" ::: "memory");  // keep LDS weight reads inside the loop (see fwd_job)
     const int64_t p = t * 16 + i;
@@ -870,11 +871,11 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
     unsigned mlo = 0, mhi = 0;
     if (valid) {
       if constexpr (KIND == K_COLOR) {
-        dout[0] = ctx.grgb[p * 3 + 0];
-        dout[1] = ctx.grgb[p * 3 + 1];
-        dout[2] = ctx.grgb[p * 3 + 2];
+        dout[0] = ctx.grgb[p * 3 + 0] * dscale;
+        dout[1] = ctx.grgb[p * 3 + 1] * dscale;
+        dout[2] = ctx.grgb[p * 3 + 2] * dscale;
       } else {
-        dout[0] = ctx.gocc[p];
+        dout[0] = ctx.gocc[p] * dscale;
       }
       const uint2 m = *reinterpret_cast<const uint2*>(rec + RC::M + 2 * g);
       mlo = m.x;

@@ -54,6 +54,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x < MAX_JOBS && c.range_flag) c.range_flag[threadIdx.x] = 0u;  // for k_mlp_fwd
+  if (blockIdx.x == 0 && threadIdx.x == 0 && c.fuse_bwd) *c.loss_out = 0.0;  // k_composite_fwd_loss adds into it
   float dmax_blk = 0.f;
   if (c.dmax_local) {  // torch.max(gt_depth) over the whole batch, by every workgroup (N small)
     __shared__ float red[RAY_WAVES];
@@ -251,51 +252,41 @@ __device__ __forceinline__ float wsum_f(float v) {
   return v;
 }
 
-__global__ void __launch_bounds__(256) k_composite_fwd(const RayCtx c) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
-  if (r >= c.N) return;
-  SampleState s;
-  sample_state(c, r, lane, s);
-  const float cr = wsum_f(s.w * s.rgb[0]);
-  const float cg = wsum_f(s.w * s.rgb[1]);
-  const float cb = wsum_f(s.w * s.rgb[2]);
-  const double depth = wsum_d((double)s.w * s.z);
+// raw2outputs_nerf_color's outputs of ray r (common.py:248-256): depth, var, colour
+__device__ __forceinline__ void composite_fwd_ray(const RayCtx& c, int64_t r, int lane, const SampleState& s,
+                                                  double& depth, float (&col)[3]) {
+  col[0] = wsum_f(s.w * s.rgb[0]);
+  col[1] = wsum_f(s.w * s.rgb[1]);
+  col[2] = wsum_f(s.w * s.rgb[2]);
+  depth = wsum_d((double)s.w * s.z);
   const double tmp = s.z - depth;
   const double var = wsum_d(lane < c.S ? ((double)s.w * tmp) * tmp : 0.0);
   if (c.weights_out && lane < c.S) c.weights_out[r * c.S + lane] = s.w;
   if (lane == 0) {
     c.depth[r] = depth;
     c.var[r] = var;
-    c.color[r * 3 + 0] = cr;
-    c.color[r * 3 + 1] = cg;
-    c.color[r * 3 + 2] = cb;
+    c.color[r * 3 + 0] = col[0];
+    c.color[r * 3 + 1] = col[1];
+    c.color[r * 3 + 2] = col[2];
   }
 }
 
-__global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
+__global__ void __launch_bounds__(256) k_composite_fwd(const RayCtx c) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
   if (r >= c.N) return;
-  const bool act = lane < c.S;
   SampleState s;
   sample_state(c, r, lane, s);
-  const double depth = wsum_d((double)s.w * s.z);
-  double gD = c.g_depth ? c.g_depth[r] : 0.0;
-  const double gV = c.g_var ? c.g_var[r] : 0.0;
-  float gC[3] = {0.f, 0.f, 0.f};
-  if (c.g_color) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gC[k] = c.g_color[r * 3 + k];
-  }
-  if (c.loss && c.g_loss) {  // the fused loss's contribution (k_loss)
-    const double gl = *c.g_loss;
-    gD = gD + gl * c.coef_d[r];
-    if (c.loss_flags & NC_LOSS_COLOR) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) gC[k] = gC[k] + (float)gl * c.coef_c[r * 3 + k];
-    }
-  }
+  double depth;
+  float col[3];
+  composite_fwd_ray(c, r, lane, s, depth, col);
+}
+
+// composite backward of ray r from the upstream (gD, gV, gC) of its depth / var / colour
+// (common.py:215-256 in reverse): writes d loss / d raw of its samples (gocc, grgb)
+__device__ __forceinline__ void composite_bwd_core(const RayCtx& c, int64_t r, int lane, const SampleState& s,
+                                                   double depth, double gD, double gV, const float (&gC)[3]) {
+  const bool act = lane < c.S;
   // var = sum w (z-D)^2, D = sum w z  (common.py:253-255)
   const double tmp = s.z - depth;
   const double gtmp = act ? 2.0 * gV * (double)s.w * tmp : 0.0;
@@ -340,6 +331,31 @@ __global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
       for (int k = 0; k < 3; ++k) c.grgb[p * 3 + k] = gC[k] * s.w;
     }
   }
+}
+
+__global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
+  if (r >= c.N) return;
+  SampleState s;
+  sample_state(c, r, lane, s);
+  const double depth = wsum_d((double)s.w * s.z);
+  double gD = c.g_depth ? c.g_depth[r] : 0.0;
+  const double gV = c.g_var ? c.g_var[r] : 0.0;
+  float gC[3] = {0.f, 0.f, 0.f};
+  if (c.g_color) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gC[k] = c.g_color[r * 3 + k];
+  }
+  if (c.loss && c.g_loss) {  // the fused loss's contribution (k_loss)
+    const double gl = *c.g_loss;
+    gD = gD + gl * c.coef_d[r];
+    if (c.loss_flags & NC_LOSS_COLOR) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gC[k] = gC[k] + (float)gl * c.coef_c[r * 3 + k];
+    }
+  }
+  composite_bwd_core(c, r, lane, s, depth, gD, gV, gC);
 }
 
 // ---------------------------------------------------------------------------
@@ -499,6 +515,71 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_composite_fwd_loss -- NC_LOSS_MAPPER with a backward to come (RayCtx::fuse_bwd):
+// the mapper loss needs no batch-wide statistic, so its per-ray derivatives are known
+// as soon as the ray is composited.  One pass per ray does k_composite_fwd, k_loss's
+// NC_LOSS_MAPPER terms (the same expressions) and k_composite_bwd for d loss = 1;
+// k_mlp_dx multiplies by the actual d loss (MlpCtx::dout_scale), so the backward skips
+// k_composite_bwd (and the forward k_loss).  coef_d / coef_c are still written for a
+// backward that also receives depth / var / colour gradients.  The loss value: the
+// workgroup's 16 rays summed in wave order, one float64 atomic per workgroup into
+// loss_out (zeroed by k_ray_setup) -- the last bits depend on the workgroups' order;
+// NC_DETERMINISTIC keeps k_loss's fixed-order sum.
+// ---------------------------------------------------------------------------
+constexpr int FUSED_RAYS = 16;  // rays (waves) per workgroup: 63 atomics at C2
+
+__global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const RayCtx c) {
+  __shared__ double part[FUSED_RAYS][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * FUSED_RAYS + wv;
+  const bool col_term = (c.loss_flags & NC_LOSS_COLOR) != 0;
+  double ld = 0.0, lc = 0.0;
+  if (r < c.N) {
+    SampleState s;
+    sample_state(c, r, lane, s);
+    double depth;
+    float col[3];
+    composite_fwd_ray(c, r, lane, s, depth, col);
+    const float gt = c.loss_depth[r];
+    const bool m = gt > 0.f;
+    const double diff = (double)gt - depth;
+    const double coef = m ? -sgn_d(diff) : 0.0;
+    ld = m ? fabs(diff) : 0.0;
+    float gC[3] = {0.f, 0.f, 0.f};
+    if (col_term) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float dc = c.loss_color[r * 3 + k] - col[k];
+        lc += (double)fabsf(dc);  // the mapper's colour term is unmasked
+        gC[k] = -(c.w_color * sgn_f(dc));
+      }
+    }
+    if (lane == 0) {
+      c.coef_d[r] = coef;
+      if (col_term) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) c.coef_c[r * 3 + k] = gC[k];
+      }
+    }
+    composite_bwd_core(c, r, lane, s, depth, coef, 0.0, gC);
+  }
+  if (lane == 0) {
+    part[wv][0] = ld;
+    part[wv][1] = lc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double d = 0.0, cs = 0.0;
+    for (int w = 0; w < FUSED_RAYS; ++w) {
+      d += part[w][0];
+      cs += part[w][1];
+    }
+    if (col_term) d = d + (double)(c.w_color * (float)cs);
+    atomicAdd(c.loss_out, d);
+  }
+}
+
 __device__ __forceinline__ void ray_grads_body(const RayCtx& c, int64_t block) {
   const int lane = threadIdx.x & 63;
   const int64_t r = block * RAY_WAVES + (threadIdx.x >> 6);
@@ -648,6 +729,11 @@ int launch_ray_setup(const RayCtx& c, hipStream_t s) {
 }
 int launch_composite_fwd(const RayCtx& c, hipStream_t s) {
   hipLaunchKernelGGL(k_composite_fwd, dim3(ray_blocks(c.N)), dim3(256), 0, s, c);
+  return (int)hipGetLastError();
+}
+int launch_composite_fwd_loss(const RayCtx& c, hipStream_t s) {
+  hipLaunchKernelGGL(k_composite_fwd_loss, dim3((unsigned)((c.N + FUSED_RAYS - 1) / FUSED_RAYS)), dim3(64 * FUSED_RAYS), 0,
+                     s, c);
   return (int)hipGetLastError();
 }
 int launch_composite_bwd(const RayCtx& c, hipStream_t s) {

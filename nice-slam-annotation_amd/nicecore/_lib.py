@@ -246,7 +246,7 @@ KERNEL_IDS = {"k_depth_max": 0, "k_ray_setup": 1, "k_mlp_fwd": 2, "k_composite_f
               "k_sample_rays": 16, "k_sample_pose_grad": 17, "k_frustum_mask": 18,
               "k_rows_clear": 19, "k_rows_merge": 20, "k_rows_compact": 21,
               "k_param_ray_reduce": 22, "k_sample_pdf": 23, "k_adam": 24,
-              "k_imap_gemm": 25, "k_imap_fourier": 26}
+              "k_imap_gemm": 25, "k_imap_fourier": 26, "k_grid_rows": 27, "k_composite_fwd_loss": 28}
 
 
 class KernelTimer:

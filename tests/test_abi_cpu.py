@@ -72,6 +72,15 @@ def test_grid_rows_argument_errors(lib):
     assert lib.nc_grid_rows(ctypes.byref(a), None) == 0  # nothing to move
 
 
+def test_kernel_timer_ids_match_library(lib):
+    """KernelTimer's name -> id table is the library's own (nc_kernel_name), every id."""
+    lib.nc_kernel_name.restype = ctypes.c_char_p
+    n = lib.nc_timing_stop(None, None, 0)
+    names = {lib.nc_kernel_name(i).decode(): i for i in range(n)}
+    assert names == L.KERNEL_IDS
+    assert n <= 32  # one bit per kernel in nc_timing_start's mask
+
+
 def test_param_counts_match_modules(lib):
     m = D.build_default_nice(seed=0)
     mods = [m.coarse_decoder, m.middle_decoder, m.fine_decoder, m.color_decoder]

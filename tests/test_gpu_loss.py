@@ -193,6 +193,25 @@ def test_fused_loss_upstream_scale():
 
 
 @pytest.mark.gpu
+def test_fused_loss_with_output_gradients():
+    """The mapper loss's forward writes d raw for d loss = 1 (k_composite_fwd_loss); a
+    backward that also receives depth / colour gradients runs k_composite_bwd on the
+    forward's loss coefficients instead: both must equal the unfused statement."""
+    rec, stage, model, g, ro, rd, r = _setup("color_depth")
+    gt, gtc = rec["gt_depth"].cuda(), rec["gt_color"].cuda()
+    d1, v1, c1, L1 = r.render_batch_loss(g, model, rd, ro, "cuda", stage, gt, gtc, loss="mapper", color_term=True)
+    (L1 + 0.5 * d1.sum() + (c1 * c1).sum()).backward()
+    G1 = _grads(model, g, ro, rd)
+    d2, v2, c2 = r.render_batch_ray(g, model, rd, ro, "cuda", stage, gt)
+    L2 = _oracle_loss("mapper", d2, v2, c2, gt, gtc, True, False)
+    (L2 + 0.5 * d2.sum() + (c2 * c2).sum()).backward()
+    G2 = _grads(model, g, ro, rd)
+    assert set(G1) == set(G2)
+    bad = {k: rel_err(G1[k].cpu(), G2[k].cpu()) for k in G1 if rel_err(G1[k].cpu(), G2[k].cpu()) > 1e-6}
+    assert not bad, bad
+
+
+@pytest.mark.gpu
 def test_no_weight_grad_flag_is_enforced(monkeypatch):
     """NC_NO_WEIGHT_GRAD(kind) (include/nicecore.h) spares the forward's activation records
     of a decoder; a backward that then asks for that decoder's weight gradient must fail
