@@ -574,7 +574,12 @@ int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipSt
   if (!m.rec) return fail(-1, "nicecore: backward needs a forward run with NC_SAVE_FOR_BACKWARD");
   const int dx_x = fwd_grid_x(P, m.n_jobs, 1);
   if (m.bslab && dx_x != m.bslab_rows) return fail(-1, "nicecore: k_mlp_dx grid differs from its workspace rows");
-  if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, dx_x, s); }), "k_mlp_dx")) return e;
+  bool vec = true;  // every grid k_mlp_dx reads is channels-last (device grid_vec_ok)
+  for (int j = 0; j < m.n_jobs; ++j) vec = vec && host_vec_ok(m.grids[m.jobs[j].kind]);
+#ifdef NC_DX_NO_VEC  // A/B: the generic (any-stride) k_mlp_dx instantiation
+  vec = false;
+#endif
+  if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, dx_x, vec, s); }), "k_mlp_dx")) return e;
   bool any_grid = false;
   for (int j = 0; j < m.n_jobs; ++j) any_grid |= m.jobs[j].need_grid != 0;
   if (m.dfeat && any_grid)

@@ -311,6 +311,40 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
   }
 }
 
+// Two channels-last lookups (the fine decoder's [fine | middle]) with all 16 corners'
+// loads in flight before either is summed: one memory round trip instead of two.  Each
+// lookup is accumulated exactly as gather8 (bit-identical).
+__device__ __forceinline__ void gather8x2(const nc_grid& G1, const Corners& c1, const nc_grid& G2, const Corners& c2,
+                                          int g, float out1[8], float out2[8]) {
+  float v[2][8][8];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const nc_grid& G = q == 0 ? G1 : G2;
+    const Corners& c = q == 0 ? c1 : c2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float* base = G.data + c.off[k];  // off = 0 for out-of-bounds corners
+      const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
+      const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
+      v[q][k][0] = a.x; v[q][k][1] = a.y; v[q][k][2] = a.z; v[q][k][3] = a.w;
+      v[q][k][4] = b.x; v[q][k][5] = b.y; v[q][k][6] = b.z; v[q][k][7] = b.w;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const Corners& c = q == 0 ? c1 : c2;
+    float* out = q == 0 ? out1 : out2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool in = (c.inb >> k) & 1u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[q][k][j] * c.w[k] : 0.f);
+    }
+  }
+}
+
 // gather8 for channels-last grids with half the registers: two batches of 4 corners
 // (offsets from the corner-0 voxel, not Corners::off), same corner order and
 // association, so the result is bit-identical to gather8 / k_grid_gather

@@ -253,7 +253,7 @@ int rec_stride(int kind);  // floats per point of a decoder's [forward | backwar
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s);  // grid = c.fwd_off[n_jobs]
 int decoder_macs(int kind);  // multiply-adds per point of one decoder's forward
 int fwd_tile_cost(int kind);  // relative k_mlp_fwd time per tile (split of its workgroups over the jobs)
-int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s);
+int launch_mlp_dx(const MlpCtx& c, int grid_x, bool vec, hipStream_t s);  // vec: all job grids channels-last
 int launch_mlp_dw(const MlpCtx& c, hipStream_t s);
 int launch_grid_gather(const MlpCtx& c, hipStream_t s);
 int rec_feat_offset(int kind);  // float offset of the features inside a point record
@@ -266,11 +266,12 @@ int64_t max_param_count();
 #define NC_FWD_THREADS 768
 #endif
 #ifndef NC_FWD_THREADS_FUSED
-#define NC_FWD_THREADS_FUSED 512
+#define NC_FWD_THREADS_FUSED 768
 #endif
 constexpr int FWD_TILES = NC_FWD_TILES;      // 16-point tiles per wave sharing the weight fragments
 constexpr int FWD_THREADS = NC_FWD_THREADS;  // k_mlp_fwd<false>: waves per workgroup x 64 (157 VGPRs)
-// k_mlp_fwd<true> (trilinear lookups fused): 8 waves, 200 VGPRs, spill-free (12 waves: 39 spills)
+// k_mlp_fwd<true> (trilinear lookups fused): 12 waves (3 per SIMD, 168 VGPRs, 6 spills) since its
+// lookups gather every corner in one round trip (172 VGPRs at 8 waves; fwd 98.5 -> 89.6 us at C2)
 constexpr int FWD_THREADS_FUSED = NC_FWD_THREADS_FUSED;
 __host__ __device__ constexpr int fwd_threads(bool fuse) { return fuse ? FWD_THREADS_FUSED : FWD_THREADS; }
 #ifndef NC_DX_THREADS

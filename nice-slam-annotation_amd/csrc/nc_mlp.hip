@@ -695,6 +695,7 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
       R[t].pf[0] = nf[t].x; R[t].pf[1] = nf[t].y; R[t].pf[2] = nf[t].z;
       if constexpr (FUSE) {
         const float xyz[3] = {nx[t].x, nx[t].y, nx[t].z};
+#ifdef NC_FWD_GATHER_B2  // A/B: two batches of 4 corners per lookup (fewer registers, more round trips)
         {
           const nc_grid& G = ctx.grids[KIND];
           Corners co;
@@ -707,6 +708,23 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
           make_corners(G, xyz, co);
           gather8_b2(G, co, g, R[t].c + 8);
         }
+#else
+        // every corner of the tile's lookups in flight at once (the MLP's registers are
+        // free here): one memory round trip per tile
+        if constexpr (KIND == K_FINE) {  // [fine | middle]: + the no-grad grid_middle lookup
+          const nc_grid& G1 = ctx.grids[K_FINE];
+          const nc_grid& G2 = ctx.grids[K_MID];
+          Corners c1, c2;
+          make_corners(G1, xyz, c1);
+          make_corners(G2, xyz, c2);
+          gather8x2(G1, c1, G2, c2, g, R[t].c, R[t].c + 8);
+        } else {
+          const nc_grid& G = ctx.grids[KIND];
+          Corners co;
+          make_corners(G, xyz, co);
+          gather8<true>(G, co, g, R[t].c);
+        }
+#endif
       } else {
 #pragma unroll
         for (int q = 0; q < CQ; ++q) {
@@ -845,7 +863,10 @@ constexpr int DX_BACC = DX_SLICE_BASE + (DX_THREADS / 64) * SCAT_FLOATS;
 constexpr int DX_LDS_FLOATS = DX_BACC + (DX_THREADS / 64) * DX_BSLAB;
 static_assert(DX_LDS_FLOATS * 4 <= 160 * 1024, "dX LDS budget");
 
-template <int KIND, bool JAC>
+// VEC: every grid of the launch is channels-last with float4-aligned rows (the host
+// checked), so the strided-channel trilinear path is not compiled in (its per-channel
+// offsets were most of the kernel's register spills)
+template <int KIND, bool JAC, bool VEC>
 __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float* lds) {
   using N = Net<KIND>;
   using RC = Rec<KIND>;
@@ -999,10 +1020,10 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
             gi[a] = lo.x * dcv[0] + lo.y * dcv[1] + lo.z * dcv[2] + lo.w * dcv[3] +
                     hi.x * dcv[4] + hi.y * dcv[5] + hi.z * dcv[6] + hi.w * dcv[7];
           }
-        } else if (grid_vec_ok(G)) {
+        } else if (VEC || grid_vec_ok(G)) {
           grid_coord_grad<true>(G, co, dcv, g, gi);
         } else {
-          grid_coord_grad<false>(G, co, dcv, g, gi);
+          if constexpr (!VEC) grid_coord_grad<false>(G, co, dcv, g, gi);
         }
         const float gm[3] = {co.gmx, co.gmy, co.gmz};
         const nc_decoder_params& D = ctx.dec[KIND];
@@ -1048,16 +1069,16 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
 
 // JAC: the coordinate gradient from the forward's saved Jacobian (NC_SAVE_POINT_JACOBIAN);
 // its own instantiation, so the corner re-read path's registers do not weigh on it
-template <bool JAC>
+template <bool JAC, bool VEC>
 __global__ void __launch_bounds__(DX_THREADS) k_mlp_dx(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Job job = pick_job(ctx.jobs, blockIdx.y);
   if (!job.need_dw && !job.need_grid && !job.need_coord) return;
   switch (job.kind) {
-    case K_COARSE: dx_job<K_COARSE, JAC>(ctx, job, lds); break;
-    case K_MID: dx_job<K_MID, JAC>(ctx, job, lds); break;
-    case K_FINE: dx_job<K_FINE, JAC>(ctx, job, lds); break;
-    default: dx_job<K_COLOR, JAC>(ctx, job, lds); break;
+    case K_COARSE: dx_job<K_COARSE, JAC, VEC>(ctx, job, lds); break;
+    case K_MID: dx_job<K_MID, JAC, VEC>(ctx, job, lds); break;
+    case K_FINE: dx_job<K_FINE, JAC, VEC>(ctx, job, lds); break;
+    default: dx_job<K_COLOR, JAC, VEC>(ctx, job, lds); break;
   }
 }
 
@@ -1429,9 +1450,10 @@ int mlp_blocks_per_cu(int which) {
       set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<true>, FWD_THREADS_FUSED, mlp_fwd_lds_bytes());
     } else if (which == 1) {
-      set_lds(k_mlp_dx<true>, mlp_dx_lds_bytes());
-      set_lds(k_mlp_dx<false>, mlp_dx_lds_bytes());
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dx<true>, DX_THREADS, mlp_dx_lds_bytes());
+      set_lds(k_mlp_dx<true, false>, mlp_dx_lds_bytes());
+      set_lds(k_mlp_dx<false, false>, mlp_dx_lds_bytes());
+      set_lds(k_mlp_dx<false, true>, mlp_dx_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dx<true, false>, DX_THREADS, mlp_dx_lds_bytes());
     } else {
       set_lds(k_mlp_dw, mlp_dw_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_dw, DW_THREADS, mlp_dw_lds_bytes());
@@ -1467,7 +1489,10 @@ int fwd_tile_cost(int kind) {
 #endif
 }
 
-constexpr int EXACT_WGS_PER_JOB = 16;
+#ifndef NC_EXACT_WGS
+#define NC_EXACT_WGS 16
+#endif
+constexpr int EXACT_WGS_PER_JOB = NC_EXACT_WGS;
 
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
   static int attr = -1;
@@ -1501,14 +1526,19 @@ int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
 
 int mlp_dx_lds_bytes() { return DX_LDS_FLOATS * 4; }
 
-int launch_mlp_dx(const MlpCtx& c, int grid_x, hipStream_t s) {
+int launch_mlp_dx(const MlpCtx& c, int grid_x, bool vec, hipStream_t s) {
   static int attr = -1;
-  if (attr != 0 && (attr = set_lds(k_mlp_dx<true>, mlp_dx_lds_bytes()) | set_lds(k_mlp_dx<false>, mlp_dx_lds_bytes())) != 0)
+  if (attr != 0 && (attr = set_lds(k_mlp_dx<true, false>, mlp_dx_lds_bytes()) |
+                           set_lds(k_mlp_dx<false, false>, mlp_dx_lds_bytes()) |
+                           set_lds(k_mlp_dx<false, true>, mlp_dx_lds_bytes())) != 0)
     return attr;
+  const dim3 grid(grid_x, c.n_jobs);
   if (c.jac)
-    hipLaunchKernelGGL(k_mlp_dx<true>, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
+    hipLaunchKernelGGL((k_mlp_dx<true, false>), grid, dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
+  else if (vec)
+    hipLaunchKernelGGL((k_mlp_dx<false, true>), grid, dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
   else
-    hipLaunchKernelGGL(k_mlp_dx<false>, dim3(grid_x, c.n_jobs), dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
+    hipLaunchKernelGGL((k_mlp_dx<false, false>), grid, dim3(DX_THREADS), mlp_dx_lds_bytes(), s, c);
   return (int)hipGetLastError();
 }
 

@@ -55,6 +55,16 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x < MAX_JOBS && c.range_flag) c.range_flag[threadIdx.x] = 0u;  // for k_mlp_fwd
   if (blockIdx.x == 0 && threadIdx.x == 0 && c.fuse_bwd) *c.loss_out = 0.0;  // k_composite_fwd_loss adds into it
+  // this ray's inputs first: their loads overlap the batch-max loop below
+  const bool live = r < c.N;
+  const int64_t rr = live ? r : 0;
+  double o[3], d[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    o[k] = (double)c.rays_o[rr * 3 + k];
+    d[k] = (double)c.rays_d[rr * 3 + k];
+  }
+  const float gd_in = (c.gt_depth && c.N > 0) ? c.gt_depth[rr] : 0.f;
   float dmax_blk = 0.f;
   if (c.dmax_local) {  // torch.max(gt_depth) over the whole batch, by every workgroup (N small)
     __shared__ float red[RAY_WAVES];
@@ -73,13 +83,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
     for (int w = 1; w < RAY_WAVES; ++w) m = (red[w] > m || isnan(red[w])) ? red[w] : m;
     dmax_blk = m;
   }
-  if (r >= c.N) return;
-  double o[3], d[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    o[k] = (double)c.rays_o[r * 3 + k];
-    d[k] = (double)c.rays_d[r * 3 + k];
-  }
+  if (!live) return;
   // Renderer.py:139-152: far_bb = min_axis(max(t0, t1)) + 0.01 (no grad, float64)
   double far_bb = 0.0;
 #pragma unroll
@@ -94,7 +98,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   double far = far_bb;
   float gd = 0.f, dmax = 0.f;
   if (has_depth) {
-    gd = c.gt_depth[r];
+    gd = gd_in;
     dmax = c.dmax_local ? dmax_blk : *c.depth_max;
     const double hi = (double)(dmax * 1.2f);  // torch.max(gt_depth*1.2) (float32)
     double v = far_bb < 0.0 ? 0.0 : far_bb;   // torch.clamp(far_bb, 0, hi)
@@ -527,7 +531,10 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
 // loss_out (zeroed by k_ray_setup) -- the last bits depend on the workgroups' order;
 // NC_DETERMINISTIC keeps k_loss's fixed-order sum.
 // ---------------------------------------------------------------------------
-constexpr int FUSED_RAYS = 16;  // rays (waves) per workgroup: 63 atomics at C2
+#ifndef NC_FUSED_RAYS
+#define NC_FUSED_RAYS 16
+#endif
+constexpr int FUSED_RAYS = NC_FUSED_RAYS;  // rays (waves) per workgroup: 63 atomics at C2
 
 __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const RayCtx c) {
   __shared__ double part[FUSED_RAYS][2];

@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.join(REPO, "nice-slam-annotation_amd"))
 DBG = os.path.join(REPO, "dbg")
 VARIANTS = {
     "base": [],
+    "cur": [],
     "no_trig": ["-DNC_ABL_NO_TRIG"],
     "no_recstore": ["-DNC_ABL_NO_RECSTORE"],
     "no_mask": ["-DNC_ABL_NO_MASK"],
@@ -38,6 +39,13 @@ VARIANTS = {
     "dw_no_mfma": ["-DNC_ABL_DW_NO_MFMA"],
     "mfma_f32": ["-DNC_MFMA_F32"],
     "no_zero_fill": ["-DNC_ABL_NO_ZERO_FILL"],
+    "fwd_no_stores": ["-DNC_ABL_NO_ZERO_FILL", "-DNC_ABL_NO_RECSTORE"],
+    "exact1": ["-DNC_EXACT_WGS=1"],
+    "fwd_b2": ["-DNC_FWD_GATHER_B2"],
+    "dx_novec": ["-DNC_DX_NO_VEC"],
+    "exact4": ["-DNC_EXACT_WGS=4"],
+    "fused4": ["-DNC_FUSED_RAYS=4"],
+    "fused8": ["-DNC_FUSED_RAYS=8"],
     "fwd_t2_512": ["-DNC_FWD_TILES=2", "-DNC_FWD_THREADS=512"],
     "fwd_t1_1024": ["-DNC_FWD_THREADS=1024"],
     "fwd_t2_768": ["-DNC_FWD_TILES=2"],
