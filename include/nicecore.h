@@ -173,7 +173,12 @@ typedef struct nc_render_args {
   /* fused rendering loss (loss != NC_LOSS_NONE): forward writes *loss_out (float64
    * device scalar, the reference's value incl. its float32 colour sum); backward adds
    * (*g_loss) * d loss / d (depth, colour) to g_depth / g_color (uncertainty enters the
-   * tracker loss detached, as in the reference). */
+   * tracker loss detached, as in the reference).  NC_LOSS_MAPPER with
+   * NC_SAVE_FOR_BACKWARD (and not NC_DETERMINISTIC): the forward also forms the loss's
+   * d raw for d loss = 1 and the backward scales it by *g_loss when that is the only
+   * upstream gradient (no k_loss / k_composite_bwd); *loss_out is then a sum of float64
+   * per-workgroup partials whose last bits depend on their order (NC_DETERMINISTIC: fixed
+   * order). */
   int32_t loss;             /* NC_LOSS_* */
   int32_t loss_flags;       /* NC_LOSS_COLOR | NC_LOSS_DYNAMIC */
   double w_color;           /* w_color_loss (applied in float32, as the reference) */

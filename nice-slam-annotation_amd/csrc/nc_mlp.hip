@@ -969,7 +969,11 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
           dpf[1] = dpf[1] + B[EMBP + m] * dx4[r];
           dpf[2] = dpf[2] + B[2 * EMBP + m] * dx4[r];
         }
+#ifdef NC_ABL_DX_NO_BGRAD  // timing-only ablation: no Fourier-B weight gradient in dx
+        if (false) {
+#else
         if (need_dw) {  // wave-uniform
+#endif
           // (c, r) = q: the row's 16-point sum of p.float()[c] * dx[16 t + 4 g + r]; lane i
           // of the row keeps sum q = i (one live sum at a time)
           float v = 0.f;

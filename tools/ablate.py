@@ -43,6 +43,7 @@ VARIANTS = {
     "exact1": ["-DNC_EXACT_WGS=1"],
     "fwd_b2": ["-DNC_FWD_GATHER_B2"],
     "dx_novec": ["-DNC_DX_NO_VEC"],
+    "dx_no_bgrad": ["-DNC_ABL_DX_NO_BGRAD"],
     "exact4": ["-DNC_EXACT_WGS=4"],
     "fused4": ["-DNC_FUSED_RAYS=4"],
     "fused8": ["-DNC_FUSED_RAYS=8"],
