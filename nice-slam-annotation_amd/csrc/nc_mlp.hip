@@ -951,12 +951,25 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
     if constexpr (N::XYZ) {
       // dx = d emb * cos(p.float() @ B), produced 4 features at a time and reduced into
       // d p.float() = B dx without keeping all 24 live.  The weight gradient of B,
-      // d B[c][m] = sum_points p.float()[c] dx[m] (decoder.py:26-30), is summed here too:
-      // over the wave's 16 points by DPP row sums, over the workgroup's tiles by LDS
-      // adds -- instead of 384 B of dx per point written to the record for k_mlp_dw.
+      // d B[c][m] = sum_points p.float()[c] dx[m] (decoder.py:26-30), is summed here too,
+      // instead of 384 B of dx per point written to the record for k_mlp_dw: per 16-feature
+      // block t one 16 x 16 product over the tile's 16 points on the MFMA -- four
+      // v_mfma_f32_16x16x4_f32 k-steps, A = p.float() of 4 points (rows c, 0 for c >= 3),
+      // B = their dx rows transposed through this wave's LDS slice -- whose rows c < 3 are
+      // added into the wave's bacc slice (over the workgroup's tiles; summed over the
+      // waves in wave order at the end: deterministic).
       const float* B = lds + N::FB;
       const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
-      const float fc[3] = {f.x, f.y, f.z};
+      constexpr int DXB_LD = 24;  // [point][16 features] rows: 16-B aligned, 2 lanes per bank on the reads
+      float pfa[4];  // A operand of k-step s: p.float()[i] of point 4 s + g (lane i < 3)
+      if (need_dw) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int src = 4 * s4 + g;  // lane (point 4 s + g, g' = 0)
+          const float px = __shfl(f.x, src), py = __shfl(f.y, src), pz = __shfl(f.z, src);
+          pfa[s4] = i == 0 ? px : (i == 1 ? py : (i == 2 ? pz : 0.f));
+        }
+      }
 #pragma unroll
       for (int t = 0; t < 6; ++t) {
         float dx4[4];
@@ -974,18 +987,23 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
 #else
         if (need_dw) {  // wave-uniform
 #endif
-          // (c, r) = q: the row's 16-point sum of p.float()[c] * dx[16 t + 4 g + r]; lane i
-          // of the row keeps sum q = i (one live sum at a time)
-          float v = 0.f;
+          *reinterpret_cast<float4*>(slice + i * DXB_LD + 4 * g) = float4{dx4[0], dx4[1], dx4[2], dx4[3]};
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          floatx4 acc = zero4();
 #pragma unroll
-          for (int q = 0; q < 12; ++q) {
-            const float sq = row16_sum(fc[q >> 2] * dx4[q & 3]);
-            v = i == q ? sq : v;
+          for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(pfa[s4], slice[(4 * s4 + g) * DXB_LD + i], acc);
+          if (g == 0) {  // rows c = 0..2 of the product: feature 16 t + i of d B[c]
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              float* a = bacc + c * EMBP + 16 * t + i;
+              *a = *a + acc[c];
+            }
           }
-          if (i < 12) {  // each (c, m) of the wave belongs to one lane: plain read-add-write
-            float* a = bacc + (i >> 2) * EMBP + 16 * t + 4 * g + (i & 3);
-            *a = *a + v;
-          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before block t+1's writes
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
       }
       if (need_coord) {
