@@ -29,6 +29,7 @@ VARIANTS = {
     "dw512_16": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=16"],
     "dw256_16": ["-DNC_DW_THREADS=256", "-DNC_DW_NPTS=16"],
     "dw1024_16": ["-DNC_DW_THREADS=1024", "-DNC_DW_NPTS=16"],
+    "dw768_16": ["-DNC_DW_THREADS=768", "-DNC_DW_NPTS=16"],
     "dw512_32": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=32"],
     "dw256_32": ["-DNC_DW_THREADS=256", "-DNC_DW_NPTS=32"],
     "dw768_32": ["-DNC_DW_THREADS=768", "-DNC_DW_NPTS=32"],
