@@ -60,6 +60,7 @@ VARIANTS = {
     "dw_npts48": ["-DNC_DW_NPTS=48"],
     "no_fuse_gather": ["-DNC_NO_FUSE_GATHER"],
     "fused768": ["-DNC_FWD_THREADS_FUSED=768"],
+    "fused1024": ["-DNC_FWD_THREADS_FUSED=1024"],
     "dw_core": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_STAGE", "-DNC_ABL_DW_NO_EMB", "-DNC_ABL_DW_NO_MASKPASS",
                 "-DNC_ABL_DW_NO_LOAD"],
     "dw_none": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_STAGE", "-DNC_ABL_DW_NO_EMB", "-DNC_ABL_DW_NO_MASKPASS",
