@@ -416,6 +416,24 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
+// v of lane (lane ^ j): DPP row permutes for j < 16 (VALU, a few cycles: xor 1 / 2 are quad
+// permutes, xor 4 = quad reverse after the half-row mirror, xor 8 = half-row mirror after
+// the row mirror), ds_bpermute (__shfl_xor) across rows.  Exactly __shfl_xor's data
+// movement, so butterflies built on it keep their bits.  j must fold to a constant.
+__device__ __forceinline__ float xor_lane(float v, int j) {
+  if (j == 1) return dpp_mov<0xB1>(v);
+  if (j == 2) return dpp_mov<0x4E>(v);
+  if (j == 4) return dpp_mov<0x1B>(dpp_mov<0x141>(v));
+  if (j == 8) return dpp_mov<0x141>(dpp_mov<0x140>(v));
+  return __shfl_xor(v, j);
+}
+__device__ __forceinline__ double xor_lane(double v, int j) {
+  const long long b = __double_as_longlong(v);
+  const float lo = xor_lane(__int_as_float((int)(b & 0xffffffffll)), j);
+  const float hi = xor_lane(__int_as_float((int)(b >> 32)), j);
+  return __longlong_as_double(((long long)__float_as_int(hi) << 32) | (unsigned)__float_as_int(lo));
+}
+
 __device__ __forceinline__ float row16_sum(float v) {
   v = v + dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
   v = v + dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]

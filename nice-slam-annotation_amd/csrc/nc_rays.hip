@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
     for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
       for (int j = k >> 1; j > 0; j >>= 1) {
-        const double other = __shfl_xor(z, j);
+        const double other = xor_lane(z, j);
         const bool up = (lane & k) == 0;
         const bool lower = (lane & j) == 0;
         const bool take_min = (lower == up);
@@ -247,12 +247,12 @@ __device__ __forceinline__ void sample_state(const RayCtx& c, int64_t r, int lan
 
 __device__ __forceinline__ double wsum_d(double v) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  for (int o = 32; o > 0; o >>= 1) v += xor_lane(v, o);
   return v;
 }
 __device__ __forceinline__ float wsum_f(float v) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  for (int o = 32; o > 0; o >>= 1) v += xor_lane(v, o);
   return v;
 }
 
