@@ -36,6 +36,41 @@ def camera_from_tensor(q):
     return torch.cat([R, q[4:7].reshape(3, 1)], dim=1)
 
 
+def graph_variant(args, r, grids, model, cam, sc, depth_d, color_d, bound, dev):
+    """The same iteration replayed as one hipGraph (nicecore.graph.GraphedStep, Adam
+    capturable) with the loss read back once per iteration.  There is no compaction, so
+    it is timed only when every ray passes the pre-filter (checked)."""
+    from nicecore.graph import GraphedStep
+    from nicecore.sampling import sample_frames
+    E, H, W = args.edge, sc.H, sc.W
+    cam_g = cam.detach().clone().requires_grad_(True)
+    opt_g = torch.optim.Adam([cam_g], lr=1e-3, capturable=True)
+
+    def body():
+        cam_g.grad = None
+        c2w = camera_from_tensor(cam_g)
+        ro, rd, gd, gc, inside = sample_frames(E, H - E, E, W - E, args.pixels, sc.fx, sc.fy, sc.cx, sc.cy,
+                                               c2w.unsqueeze(0), depth_d, color_d, bound=bound, device=dev)
+        d, u, c, loss = r.render_batch_loss(grids, model, rd, ro, dev, "color", gd, gc, loss="tracker",
+                                            color_term=True, w_color_loss=0.5, handle_dynamic=True)
+        loss.backward()
+        opt_g.step()
+        return loss, inside
+    step = GraphedStep(body)
+    _, inside = step()
+    if not bool(inside.all()):
+        return {"graph_error": "a ray failed the bbox pre-filter: the graph variant would skip a compaction"}
+    for _ in range(args.warmup):
+        step()[0].item()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.iters):
+        lg = step()[0].item()  # the Tracker's loss.item() sync, once per iteration
+    torch.cuda.synchronize()
+    g_ms = (time.perf_counter() - t) / args.iters * 1e3
+    return {"graph_ms_per_iteration": round(g_ms, 4), "graph_last_loss": lg}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200)
@@ -43,6 +78,9 @@ def main():
     ap.add_argument("--pixels", type=int, default=200)
     ap.add_argument("--edge", type=int, default=100)
     ap.add_argument("--scene", default="replica_room0")
+    ap.add_argument("--graph", action="store_true",
+                    help="also replay the iteration as one hipGraph (no compaction: this workload's "
+                         "rays all pass the pre-filter, which is checked)")
     args = ap.parse_args()
     import bench
     from nicecore.sampling import sample_frames, bbox_filter
@@ -67,7 +105,7 @@ def main():
     bound = sc.bound.to(dev)
     E, H, W = args.edge, sc.H, sc.W
 
-    def iteration(timed_parts=None):
+    def iteration():
         c2w = camera_from_tensor(cam)
         ro, rd, gd, gc, inside = sample_frames(E, H - E, E, W - E, args.pixels, sc.fx, sc.fy, sc.cx, sc.cy,
                                                c2w.unsqueeze(0), depth_d, color_d, bound=bound, device=dev)
@@ -106,7 +144,13 @@ def main():
         render_only()
     torch.cuda.synchronize()
     rb_ms = (time.perf_counter() - t) / args.iters * 1e3
-    print(json.dumps({"workload": f"{args.scene} Tracker iteration, {args.pixels} pixels (edge {args.edge}), "
+    graph = {}
+    if args.graph:
+        try:
+            graph = graph_variant(args, r, grids, model, cam, sc, depth_d, color_d, bound, dev)
+        except Exception as e:  # reported; the eager line stands
+            graph = {"graph_error": repr(e)[:300]}
+    print(json.dumps({**graph, "workload": f"{args.scene} Tracker iteration, {args.pixels} pixels (edge {args.edge}), "
                                   f"stage color, handle_dynamic, colour term", "rays_kept": int(ro.shape[0]),
                       "ms_per_iteration": round(it_ms, 4), "render_loss_backward_ms": round(rb_ms, 4),
                       "iterations_per_s": round(1e3 / it_ms, 1), "last_loss": lv}))
