@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 9
+#define NC_ABI_VERSION 10
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -209,6 +209,17 @@ typedef struct nc_render_args {
    * caller's uniform draws t_rand [N][n_strat] float32 (the reference's
    * torch.rand(z_vals.shape)); NULL = no perturbation. */
   const float* t_rand;
+  /* ABI v10: per-ray validity -- the callers' bbox pre-filter (src/Tracker.py:100-111,
+   * src/Mapper.py:580-596) as a mask instead of a boolean-index compaction (a host sync).
+   * A ray with ray_valid[i] == 0 is dropped: it is left out of the batch-global
+   * max(gt_depth) (Renderer.py:157, :194), of the fused loss and of the Tracker's
+   * handle_dynamic median; its depth / var / colour (and weights_out) are written as 0,
+   * it adds nothing to any grid or decoder gradient and its ray gradients are 0.  The
+   * kept rays' outputs, the loss and every gradient are those of rendering the compacted
+   * batch (up to the summation order of the float reductions).  The samples of dropped
+   * rays are still evaluated (fixed shapes: the call stays graph-capturable); non-finite
+   * sample depths / points of dropped rays are replaced by 0.  NULL = every ray kept. */
+  const uint8_t* ray_valid;
 } nc_render_args;
 
 typedef struct nc_points_args {

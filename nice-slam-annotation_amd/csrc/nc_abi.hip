@@ -544,6 +544,7 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
     c.coef_d = at<double>(ws, w.coef_d);
     c.coef_c = at<float>(ws, w.coef_c);
   }
+  c.valid = a->ray_valid;
 }
 
 int fwd_grid_x(int64_t P, int n_jobs, int which) {
@@ -710,7 +711,7 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   if (a->gt_depth && !a->depth_max) {
     if (a->n_rays <= kDmaxLocalRays) {
       rc.dmax_local = 1;  // reduced inside k_ray_setup
-    } else if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) {
+    } else if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->ray_valid, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) {
       return e;
     }
   }
@@ -1340,7 +1341,7 @@ int nc_imap_render_forward(const nc_imap_render_args* a, void* ws, size_t ws_byt
   if (a->gt_depth && !a->depth_max) {
     if (a->n_rays <= kDmaxLocalRays) {
       rc.dmax_local = 1;
-    } else if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) {
+    } else if (int e = check_hip(timed(KID_DEPTH_MAX, s, [&] { return launch_depth_max(a->gt_depth, nullptr, a->n_rays, at<float>(ws, w.dmax), s); }), "k_depth_max")) {
       return e;
     }
   }

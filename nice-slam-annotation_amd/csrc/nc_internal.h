@@ -176,7 +176,11 @@ struct RayCtx {
   float* gnorm;              // [N]
   int32_t fuse_bwd;          // NC_LOSS_MAPPER forward for a backward: k_composite_fwd_loss writes the
                              // loss's d raw for d loss = 1 (gocc / grgb); no k_loss, no k_composite_bwd
+  const uint8_t* valid;      // [N] nc_render_args.ray_valid (0 = ray dropped), or NULL
 };
+
+// ray r is kept (nc_render_args.ray_valid)
+__device__ __forceinline__ bool ray_ok(const RayCtx& c, int64_t r) { return c.valid == nullptr || c.valid[r] != 0; }
 
 // One layer GEMM of the iMAP* MLP (nc_imap.hip): C[m][n] (+)= sum_k A(m,k) B(k,n)
 struct ImapGemm {
@@ -230,7 +234,7 @@ struct ParamReduceCtx {
 constexpr int DX_BSLAB = 3 * 96;  // floats per k_mlp_dx workgroup: d B [3][EMBP]
 
 // kernels: launch wrappers (return hipError_t as int)
-int launch_depth_max(const float* gt, int64_t n, float* out, hipStream_t s);
+int launch_depth_max(const float* gt, const uint8_t* valid, int64_t n, float* out, hipStream_t s);
 int launch_ray_setup(const RayCtx& c, hipStream_t s);
 int launch_composite_fwd(const RayCtx& c, hipStream_t s);
 int launch_composite_fwd_loss(const RayCtx& c, hipStream_t s);

@@ -23,10 +23,11 @@ namespace nc {
 
 constexpr int RAY_WAVES = 4;  // rays per 256-thread workgroup
 
-__global__ void __launch_bounds__(1024) k_depth_max(const float* gt, int64_t n, float* out) {
+__global__ void __launch_bounds__(1024) k_depth_max(const float* gt, const uint8_t* valid, int64_t n, float* out) {
   __shared__ float red[16];
   float m = -INFINITY;
   for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+    if (valid && !valid[k]) continue;  // dropped rays (ray_valid) are not in the batch
     const float v = gt[k];
     m = (v > m || isnan(v)) ? v : m;
   }
@@ -70,6 +71,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
     __shared__ float red[RAY_WAVES];
     float m = -INFINITY;
     for (int64_t k = threadIdx.x; k < c.N; k += blockDim.x) {
+      if (c.valid && !c.valid[k]) continue;  // dropped rays (ray_valid) are not in the batch
       const float v = c.gt_depth[k];
       m = (v > m || isnan(v)) ? v : m;
     }
@@ -153,6 +155,8 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
       }
     }
   }
+  const bool ok = ray_ok(c, r);  // a dropped ray's samples stay finite: they feed the decoders
+  if (!ok && !isfinite(z)) z = 0.0;
   if (lane < c.S) {
     const int64_t p = r * c.S + lane;
     c.z[p] = z;
@@ -161,6 +165,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       pt[k] = o[k] + d[k] * z;  // Renderer.py:227-228
+      if (!ok && !isfinite(pt[k])) pt[k] = 0.0;
       c.pts[p * 3 + k] = pt[k];
     }
     c.pf[p] = float4{(float)pt[0], (float)pt[1], (float)pt[2], 0.f};
@@ -265,13 +270,14 @@ __device__ __forceinline__ void composite_fwd_ray(const RayCtx& c, int64_t r, in
   depth = wsum_d((double)s.w * s.z);
   const double tmp = s.z - depth;
   const double var = wsum_d(lane < c.S ? ((double)s.w * tmp) * tmp : 0.0);
-  if (c.weights_out && lane < c.S) c.weights_out[r * c.S + lane] = s.w;
+  const bool ok = ray_ok(c, r);  // a dropped ray (ray_valid) reports zeros
+  if (c.weights_out && lane < c.S) c.weights_out[r * c.S + lane] = ok ? s.w : 0.f;
   if (lane == 0) {
-    c.depth[r] = depth;
-    c.var[r] = var;
-    c.color[r * 3 + 0] = col[0];
-    c.color[r * 3 + 1] = col[1];
-    c.color[r * 3 + 2] = col[2];
+    c.depth[r] = ok ? depth : 0.0;
+    c.var[r] = ok ? var : 0.0;
+    c.color[r * 3 + 0] = ok ? col[0] : 0.f;
+    c.color[r * 3 + 1] = ok ? col[1] : 0.f;
+    c.color[r * 3 + 2] = ok ? col[2] : 0.f;
   }
 }
 
@@ -359,7 +365,11 @@ __global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
       for (int k = 0; k < 3; ++k) gC[k] = gC[k] + (float)gl * c.coef_c[r * 3 + k];
     }
   }
-  composite_bwd_core(c, r, lane, s, depth, gD, gV, gC);
+  if (!ray_ok(c, r)) {  // a dropped ray passes no gradient on (its d raw is exactly 0)
+    gD = 0.0;
+    gC[0] = gC[1] = gC[2] = 0.f;
+  }
+  composite_bwd_core(c, r, lane, s, depth, gD, ray_ok(c, r) ? gV : 0.0, gC);
 }
 
 // ---------------------------------------------------------------------------
@@ -383,6 +393,8 @@ __global__ void __launch_bounds__(256) k_composite_bwd(const RayCtx c) {
 // ---------------------------------------------------------------------------
 constexpr int LOSS_THREADS = 1024;
 constexpr int LOSS_KEYS = 4096;  // rays whose median keys are held in LDS (32 KB)
+// key of a dropped ray in the cached median keys: a NaN bit pattern, never a real tmp's
+constexpr unsigned long long KEY_DROPPED = ~0ull - 1ull;
 
 __device__ __forceinline__ double sgn_d(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
 __device__ __forceinline__ float sgn_f(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
@@ -408,17 +420,30 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
     // up to LOSS_KEYS rays (the Tracker's batches) the keys are formed once into LDS
     // (~0 marks NaN); beyond, every pass recomputes tmp from depth / var
     __shared__ unsigned long long skey[LOSS_KEYS];
+    __shared__ unsigned vpart[LOSS_THREADS / 64];
     const bool cached = c.N <= LOSS_KEYS;
+    if (c.valid) {  // the median is over the kept rays only (ray_valid: the compacted batch)
+      unsigned cnt = 0;
+      for (int64_t r = tid; r < c.N; r += LOSS_THREADS) cnt += c.valid[r] != 0 ? 1u : 0u;
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+      if ((tid & 63) == 0) vpart[tid >> 6] = cnt;
+      __syncthreads();
+    }
     if (tid == 0) {
+      long long nv = (long long)c.N;
+      if (c.valid) {
+        nv = 0;
+        for (int w = 0; w < LOSS_THREADS / 64; ++w) nv += vpart[w];
+      }
       sel_prefix = 0ull;
-      sel_k = (long long)((c.N - 1) / 2);
+      sel_k = (nv - 1) / 2;
       any_nan = 0;
     }
     if (cached) {
       for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
         double diff, s;
         const double t = tracker_tmp(c, r, diff, s);
-        skey[r] = isnan(t) ? ~0ull : (unsigned long long)__double_as_longlong(t);
+        skey[r] = !ray_ok(c, r) ? KEY_DROPPED : isnan(t) ? ~0ull : (unsigned long long)__double_as_longlong(t);
       }
     }
     unsigned long long pmask = 0ull;
@@ -434,7 +459,9 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
             any_nan = 1;
             continue;
           }
+          if (key == KEY_DROPPED) continue;
         } else {
+          if (!ray_ok(c, r)) continue;
           double diff, s;
           const double t = tracker_tmp(c, r, diff, s);
           if (isnan(t)) {
@@ -475,6 +502,14 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
   }
   double sd = 0.0, sc = 0.0;
   for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
+    if (!ray_ok(c, r)) {  // a dropped ray (ray_valid) is not in the loss
+      c.coef_d[r] = 0.0;
+      if (col) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) c.coef_c[r * 3 + k] = 0.f;
+      }
+      continue;
+    }
     const float gt = c.loss_depth[r];
     bool m = gt > 0.f;
     double val, coef;
@@ -548,13 +583,14 @@ __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const Ra
     double depth;
     float col[3];
     composite_fwd_ray(c, r, lane, s, depth, col);
+    const bool ok = ray_ok(c, r);  // a dropped ray (ray_valid) is not in the loss
     const float gt = c.loss_depth[r];
-    const bool m = gt > 0.f;
+    const bool m = ok && gt > 0.f;
     const double diff = (double)gt - depth;
     const double coef = m ? -sgn_d(diff) : 0.0;
     ld = m ? fabs(diff) : 0.0;
     float gC[3] = {0.f, 0.f, 0.f};
-    if (col_term) {
+    if (col_term && ok) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const float dc = c.loss_color[r * 3 + k] - col[k];
@@ -591,8 +627,8 @@ __device__ __forceinline__ void ray_grads_body(const RayCtx& c, int64_t block) {
   const int lane = threadIdx.x & 63;
   const int64_t r = block * RAY_WAVES + (threadIdx.x >> 6);
   if (r >= c.N) return;
-  const bool act = lane < c.S;
-  const int64_t p = r * c.S + (act ? lane : 0);
+  const bool act = lane < c.S && ray_ok(c, r);  // a dropped ray's gradients are 0
+  const int64_t p = r * c.S + (lane < c.S ? lane : 0);
   double dp[3] = {0.0, 0.0, 0.0};
   if (act) {
     for (int j = 0; j < c.n_jobs; ++j) {
@@ -726,8 +762,8 @@ __global__ void k_points_grads(const MlpCtx m, double* g_pts) {
 // ---- launch wrappers ----
 static inline unsigned ray_blocks(int64_t n) { return (unsigned)((n + RAY_WAVES - 1) / RAY_WAVES); }
 
-int launch_depth_max(const float* gt, int64_t n, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_depth_max, dim3(1), dim3(1024), 0, s, gt, n, out);
+int launch_depth_max(const float* gt, const uint8_t* valid, int64_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_depth_max, dim3(1), dim3(1024), 0, s, gt, valid, n, out);
   return (int)hipGetLastError();
 }
 int launch_ray_setup(const RayCtx& c, hipStream_t s) {

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 9
+NC_ABI_VERSION = 10
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
 NC_SAVE_POINT_JACOBIAN = 4
@@ -67,7 +67,8 @@ class NcRenderArgs(ctypes.Structure):
                 ("loss_depth", c_void_p), ("loss_color", c_void_p), ("loss_out", c_void_p), ("g_loss", c_void_p),
                 ("grad_zero", c_void_p), ("grad_zero_floats", c_int64),
                 ("z_extra", c_void_p), ("n_extra", c_int32), ("reserved3", c_int32),
-                ("z_out", c_void_p), ("weights_out", c_void_p), ("t_rand", c_void_p)]
+                ("z_out", c_void_p), ("weights_out", c_void_p), ("t_rand", c_void_p),
+                ("ray_valid", c_void_p)]
 
 
 class NcPointsArgs(ctypes.Structure):

@@ -32,9 +32,12 @@ def shard(rank: int, world: int, *tensors):
     return tuple(t[a:b] for t in tensors)
 
 
-def global_depth_max(gt_depth: torch.Tensor, group=None) -> torch.Tensor:
-    """max(gt_depth) over every rank's rays, as a 1-element float32 tensor."""
+def global_depth_max(gt_depth: torch.Tensor, group=None, ray_mask=None) -> torch.Tensor:
+    """max(gt_depth) over every rank's rays, as a 1-element float32 tensor; with
+    ``ray_mask`` over the kept rays only (the compacted batch of the bbox pre-filter)."""
     local = gt_depth.detach().reshape(-1).float()
+    if ray_mask is not None:  # no compaction (host sync): dropped rays count as -inf
+        local = torch.where(ray_mask.reshape(-1).bool(), local, torch.full_like(local, float("-inf")))
     m = local.max().reshape(1) if local.numel() else torch.full((1,), float("-inf"), device=local.device)
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)

@@ -22,7 +22,7 @@ def eval_points(decoders, p, c_grid, stage='middle', deterministic=None, sparse_
 
 
 def _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, n_surf,
-                       depth_max, n_importance, det, lindisp=False, t_rand=None):
+                       depth_max, n_importance, det, lindisp=False, t_rand=None, ray_valid=None):
     """Renderer.py:239-250: a forward-only first pass over the stratified (+ surface)
     samples, then sample_pdf over its weights without the first and last sample at the
     mid-points of its depths.  Returns the N_importance depths [N, n_importance]."""
@@ -33,7 +33,7 @@ def _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_st
     w = torch.empty(N, S, device=dev, dtype=torch.float32)
     plan = make_plan(stage, decoders)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": n_surf, "bound": bound, "depth_max": depth_max,
-            "z_out": z, "weights_out": w, "lindisp": lindisp, "t_rand": t_rand}
+            "z_out": z, "weights_out": w, "lindisp": lindisp, "t_rand": t_rand, "ray_valid": ray_valid}
     with torch.no_grad():
         grids = [g.detach() if g is not None else None for g in _grid_args(c)]
         NiceRenderFn.apply(spec, rays_o.detach(), rays_d.detach(),
@@ -57,7 +57,7 @@ def _t_rand(t_rand, perturb, n_rays, n_strat, device):
 
 def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_strat=32,
                 n_surf=16, depth_max=None, deterministic=None, sparse_grads=None, n_importance=0,
-                perturb=0., lindisp=False, t_rand=None, param_grads=None):
+                perturb=0., lindisp=False, t_rand=None, param_grads=None, ray_mask=None):
     """Renderer.render_batch_ray core (src/utils/Renderer.py:95-262), occupancy = True.
     Returns (depth float64 [N], uncertainty float64 [N], color float32 [N,3]).
 
@@ -81,7 +81,13 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     the differentiable render over the sorted union of both sample sets.
 
     ``param_grads``: "direct" (default) or "autograd" -- how the decoder parameters get
-    their ``.grad`` (render_fn.param_inputs)."""
+    their ``.grad`` (render_fn.param_inputs).
+
+    ``ray_mask``: optional [N] bool / uint8 device tensor, the callers' bbox pre-filter
+    (Tracker.py:100-111, Mapper.py:580-596) applied as a mask instead of ``rays[mask]``:
+    rays where it is False are dropped from the batch depth max, the loss and every
+    gradient, and report depth / uncertainty / colour 0; the kept rays get what the
+    compacted batch would (no host sync: the call stays graph-capturable)."""
     if stage == 'coarse':
         gt_depth = None
     ns = n_surf if gt_depth is not None else 0
@@ -90,11 +96,12 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     plan = make_plan(stage, decoders)
     tr = _t_rand(t_rand, perturb, rays_o.shape[0], n_strat, rays_o.device)
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
-            "deterministic": deterministic, "sparse": sparse_grads, "lindisp": bool(lindisp), "t_rand": tr}
-    if n_importance > 0:
+            "deterministic": deterministic, "sparse": sparse_grads, "lindisp": bool(lindisp), "t_rand": tr,
+            "ray_valid": ray_mask}
+    if n_importance > 0:  # sample_pdf is stochastic exactly when the stratified samples are jittered
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
-                                             depth_max, n_importance, det=(perturb == 0.),
-                                             lindisp=bool(lindisp), t_rand=tr)
+                                             depth_max, n_importance, det=(tr is None),
+                                             lindisp=bool(lindisp), t_rand=tr, ray_valid=ray_mask)
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c),
                               *param_inputs(spec, plan, rays_o.device, param_grads))
 
@@ -106,7 +113,7 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
                      target_color=None, w_color=0.2, color_term=False, handle_dynamic=False,
                      gt_depth="target", n_strat=32, n_surf=16, depth_max=None, deterministic=None,
                      sparse_grads=None, n_importance=0, perturb=0., defer_param_grads=None, lindisp=False,
-                     t_rand=None, param_grads=None):
+                     t_rand=None, param_grads=None, ray_mask=None):
     """render_rays + the rendering loss in the same launches.  Returns (depth, uncertainty,
     color, loss) with ``loss`` a float64 device scalar that backpropagates into the
     grids / decoders / rays like the reference's loss expression:
@@ -123,7 +130,8 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
     by default the target itself (the tracker and the non-coarse mapper); the coarse
     mapper renders with None.  ``defer_param_grads``: a render_fn.DeferParamGrads that
     takes the decoder weight gradients out of ``backward()`` (data-parallel overlap).
-    ``param_grads``: see render_rays."""
+    ``param_grads``, ``ray_mask``: see render_rays (a dropped ray is in neither loss term
+    nor the tracker's median)."""
     if loss not in _LOSS_KINDS:
         raise L.NiceCoreError(f"loss must be one of {sorted(_LOSS_KINDS)}")
     if handle_dynamic and loss != "tracker":
@@ -143,11 +151,11 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
             "deterministic": deterministic, "sparse": sparse_grads,
             "loss": (_LOSS_KINDS[loss], flags, w_color, target_depth, target_color if color_term else None),
-            "defer": defer_param_grads, "lindisp": bool(lindisp), "t_rand": tr}
+            "defer": defer_param_grads, "lindisp": bool(lindisp), "t_rand": tr, "ray_valid": ray_mask}
     if n_importance > 0:
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
-                                             depth_max, n_importance, det=(perturb == 0.),
-                                             lindisp=bool(lindisp), t_rand=tr)
+                                             depth_max, n_importance, det=(tr is None),
+                                             lindisp=bool(lindisp), t_rand=tr, ray_valid=ray_mask)
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c),
                               *param_inputs(spec, plan, rays_o.device, param_grads))
 

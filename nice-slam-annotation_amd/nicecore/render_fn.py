@@ -561,6 +561,15 @@ class NiceRenderFn(torch.autograd.Function):
                     or tr.device != device:
                 raise L.NiceCoreError("t_rand must be a contiguous float32 [N, n_strat] tensor on the render device")
             a.t_rand = tr.data_ptr()
+        # the callers' bbox pre-filter as a per-ray mask (ABI v10 ray_valid): dropped rays are
+        # out of the batch depth max, the loss and every gradient -- no compaction, no host sync
+        rv = spec.get("ray_valid")
+        if rv is not None:
+            rv = rv.detach().reshape(-1)
+            if rv.shape[0] != N or rv.device != device:
+                raise L.NiceCoreError("ray_mask must hold one entry per ray, on the render device")
+            rv = rv.to(torch.uint8).contiguous()
+            a.ray_valid = rv.data_ptr()
         grids = (g0, g1, g2, g3)
         gkeep = []
         for k in plan.grids:
@@ -606,7 +615,7 @@ class NiceRenderFn(torch.autograd.Function):
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
         ctx.sparse = sparse
         ctx.defer = spec.get("defer")
-        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt, zx, tr)
+        ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt, zx, tr, rv)
         a.z_out, a.weights_out = None, None  # pass-1 outputs: not rewritten by the backward
         ctx.grids = grids
         if loss is None:

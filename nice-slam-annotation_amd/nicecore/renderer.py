@@ -85,27 +85,31 @@ class Renderer(object):
         return out
 
     def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None,
-                         depth_max=None, sparse_grads=None, t_rand=None):
+                         depth_max=None, sparse_grads=None, t_rand=None, ray_mask=None):
         """Renderer.py:95-262.  Extensions: ``depth_max`` overrides the batch-global
         max(gt_depth) with a precomputed (e.g. all-reduced) device scalar;
         ``sparse_grads`` (nicecore.sparse.SparseGridGrads) takes the covered grids'
         gradients as touched-voxel rows (grids too large for a dense gradient);
-        ``t_rand`` ([N, N_samples]) gives perturb's draws instead of torch.rand."""
+        ``t_rand`` ([N, N_samples]) gives perturb's draws instead of torch.rand;
+        ``ray_mask`` ([N] bool, e.g. sampling.sample_frames' ``inside``) drops the rays the
+        callers' bbox pre-filter rejects without compacting the batch (ops.render_rays)."""
         self._check_supported()
         if gt_depth is not None:
             gt_depth = gt_depth.reshape(-1)
         if not self.nice:  # iMAP*: the scene MLP + volume density (nicecore.imap)
+            if ray_mask is not None:
+                raise NotImplementedError("ray_mask is the NICE callers' bbox pre-filter (Tracker.py:99, Mapper.py:580)")
             return _imap.render_rays(decoders, rays_o, rays_d, self.bound, gt_depth, self.N_samples,
                                      self.N_importance, depth_max)
         return render_rays(decoders, c, rays_o, rays_d, self.bound, stage, gt_depth,
                            self.N_samples, self.N_surface, depth_max, sparse_grads=sparse_grads,
                            n_importance=self.N_importance, perturb=self.perturb, lindisp=self.lindisp,
-                           t_rand=t_rand, param_grads=self.param_grads)
+                           t_rand=t_rand, param_grads=self.param_grads, ray_mask=ray_mask)
 
     def render_batch_loss(self, c, decoders, rays_d, rays_o, device, stage, gt_depth, gt_color=None,
                           loss='mapper', w_color_loss=0.2, color_term=False, handle_dynamic=False,
                           render_gt_depth='target', depth_max=None, sparse_grads=None,
-                          defer_param_grads=None, t_rand=None):
+                          defer_param_grads=None, t_rand=None, ray_mask=None):
         """render_batch_ray + the rendering loss (ops.render_rays_loss): returns
         (depth, uncertainty, color, loss).  Mapper.optimize_map:
         ``loss='mapper', color_term=(not nice) or stage == 'color',
@@ -119,7 +123,8 @@ class Renderer(object):
                                 render_gt_depth, self.N_samples, self.N_surface, depth_max,
                                 sparse_grads=sparse_grads, n_importance=self.N_importance,
                                 perturb=self.perturb, defer_param_grads=defer_param_grads,
-                                lindisp=self.lindisp, t_rand=t_rand, param_grads=self.param_grads)
+                                lindisp=self.lindisp, t_rand=t_rand, param_grads=self.param_grads,
+                                ray_mask=ray_mask)
 
     def regulation(self, c, decoders, rays_d, rays_o, gt_depth, device, stage='color', t_rand=None):
         """Renderer.py:343-409 (iMAP* only): densities of N_samples points per ray in

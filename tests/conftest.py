@@ -38,8 +38,10 @@ def load_meta():
         return json.load(f)
 
 
-def load_scene():
-    z = np.load(os.path.join(GOLDEN, "scene_tiny.npz"))
+def load_scene(which="tiny"):
+    """The golden scene: "tiny" (make_golden.py, scaled grids) or "initstd"
+    (make_golden_initstd.py, the reference's grid_init statistics)."""
+    z = np.load(os.path.join(GOLDEN, f"scene_{which}.npz"))
     bound = torch.from_numpy(z["bound"])
     grids = {k: torch.from_numpy(z[k]) for k in z.files if k.startswith("grid_")}
     params = {k[len("param/"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param/")}
@@ -52,3 +54,11 @@ def load_case(name):
 
 
 CASE_NAMES = [c["name"] for c in load_meta()["cases"]]
+
+
+def load_initstd_meta():
+    with open(os.path.join(GOLDEN, "initstd_meta.json")) as f:
+        return json.load(f)
+
+
+INITSTD_CASES = [c["name"] for c in load_initstd_meta()["cases"]]

@@ -81,8 +81,11 @@ CASES = [
 ]
 
 
-def setup():
-    """The tiny scene, the reference's model and grids as main() builds them."""
+def setup(scaled=True):
+    """The tiny scene, the reference's model and grids as main() builds them.
+    scaled=False keeps the reference's own grid_init statistics (N(0, 0.01), fine
+    N(0, 1e-4), NICE_SLAM.py:289-319) and decoder initialisers untouched: the data the
+    benchmark renders (make_golden_initstd.py)."""
     ref_config, RefRenderer, cfg = _import_reference()
     scene = S.make_scene("tiny")
     cfg['mapping']['bound'] = S.PRESETS["tiny"]["bound"]
@@ -100,6 +103,10 @@ def setup():
 
     gen = torch.Generator().manual_seed(5)
     grids = S.init_grids(scene.shapes, generator=gen)
+    if not scaled:
+        slam = types.SimpleNamespace(nice=True, bound=bound, H=scene.H, W=scene.W, fx=scene.fx,
+                                     fy=scene.fy, cx=scene.cx, cy=scene.cy)
+        return ref_config, RefRenderer, cfg, scene, model, {k: v.contiguous() for k, v in grids.items()}, bound, slam
     # Random-init decoders give occ ~ 0, i.e. alpha ~ 0.5 on every sample, so all
     # compositing weight would sit on the first samples and later samples would be
     # untested.  Scale the grids up and bias the occupancy heads negative so the

@@ -8,7 +8,7 @@ import types
 import numpy as np
 import torch
 
-from conftest import load_case, load_meta, load_scene
+from conftest import load_case, load_initstd_meta, load_meta, load_scene
 from nicecore import decoder as D
 from nicecore import scene as S
 from nicecore.renderer import Renderer
@@ -34,12 +34,18 @@ def make_renderer(bound, H=48, W=64):
 
 
 def case_stage(name):
-    c = next(c for c in load_meta()["cases"] if c["name"] == name)
+    cases = load_meta()["cases"] + load_initstd_meta()["cases"]
+    c = next(c for c in cases if c["name"] == name)
     return c["stage"], c["with_depth"]
 
 
+def scene_of(name):
+    """Golden scene a case was rendered on (make_golden.py / make_golden_initstd.py)."""
+    return "initstd" if name.startswith("initstd_") else "tiny"
+
+
 def run_case(name, device="cuda", channels_last=False, want=("rays", "grids", "params")):
-    bound, cbound, grids, params = load_scene()
+    bound, cbound, grids, params = load_scene(scene_of(name))
     rec = load_case(name)
     stage, with_depth = case_stage(name)
     model = build_model(params, bound, cbound, device)
