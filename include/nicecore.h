@@ -480,6 +480,13 @@ int nc_timing_start(uint32_t kernel_mask);
 int nc_timing_stop(double* total_ms, int64_t* launches, int max_kernels);
 const char* nc_kernel_name(int kernel_id);
 
+/* NICE_CORE_PROFILE=1 in the environment: every kernel launch of the process is event-timed
+ * on its stream (launches enqueued during a graph capture excepted) and folded into
+ * per-kernel totals; nc_profile_report prints launches / total / average per kernel to
+ * stderr (the Python binding calls it at interpreter exit).  Returns 0 (also when the
+ * flag is off), negative if an event could not be read. */
+int nc_profile_report(void);
+
 size_t nc_points_workspace_bytes(const nc_points_args* args);
 int nc_points_forward(const nc_points_args* args, void* workspace, size_t workspace_bytes,
                       void* stream);

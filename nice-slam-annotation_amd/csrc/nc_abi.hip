@@ -9,6 +9,7 @@
 // device allocation (graph-capturable).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -57,20 +58,73 @@ struct Timing {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
 } g_timing;
 
-template <typename F>
-int timed(int id, hipStream_t s, F&& launch) {
-  if (!(g_timing.mask & (1u << id))) return launch();
-  std::pair<hipEvent_t, hipEvent_t> ev;
+// NICE_CORE_PROFILE=1: every timed launch of the process is event-timed on
+// its stream and folded into per-kernel totals; nc_profile_report() prints them (the Python
+// binding calls it at exit).  Launches enqueued while the stream is being captured into a
+// graph are not timed (counted apart).  Every 2,048 pending launches the older half is
+// synchronised and folded, so a long run keeps a bounded event list.
+struct Profile {
+  int on = -1;
+  std::vector<TimedLaunch> pending;
+  double total_ms[KID_COUNT] = {};
+  int64_t launches[KID_COUNT] = {};
+  int64_t captured = 0;
+} g_prof;
+
+bool profile_on() {
+  if (g_prof.on < 0) {
+    const char* e = std::getenv("NICE_CORE_PROFILE");
+    g_prof.on = (e && e[0] == '1' && e[1] == 0) ? 1 : 0;
+  }
+  return g_prof.on == 1;
+}
+
+bool take_events(std::pair<hipEvent_t, hipEvent_t>& ev) {
   if (!g_timing.pool.empty()) {
     ev = g_timing.pool.back();
     g_timing.pool.pop_back();
-  } else {
-    if (hipEventCreate(&ev.first) != hipSuccess || hipEventCreate(&ev.second) != hipSuccess) return launch();
+    return true;
   }
-  (void)hipEventRecord(ev.first, s);
+  return hipEventCreate(&ev.first) == hipSuccess && hipEventCreate(&ev.second) == hipSuccess;
+}
+
+int prof_fold(size_t n) {  // synchronise and fold the oldest n pending launches
+  if (n > g_prof.pending.size()) n = g_prof.pending.size();
+  int rc = 0;
+  for (size_t k = 0; k < n; ++k) {
+    const TimedLaunch& t = g_prof.pending[k];
+    float ms = 0.f;
+    if (hipEventSynchronize(t.e) != hipSuccess || hipEventElapsedTime(&ms, t.b, t.e) != hipSuccess) rc = -4;
+    g_prof.total_ms[t.id] += ms;
+    g_prof.launches[t.id] += 1;
+    g_timing.pool.push_back({t.b, t.e});
+  }
+  g_prof.pending.erase(g_prof.pending.begin(), g_prof.pending.begin() + (long)n);
+  return rc;
+}
+
+template <typename F>
+int timed(int id, hipStream_t s, F&& launch) {
+  const bool t = (g_timing.mask & (1u << id)) != 0;
+  const bool p = profile_on();
+  if (!t && !p) return launch();
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+    if (p) g_prof.captured++;  // events inside a graph capture: not timed
+    return launch();
+  }
+  std::pair<hipEvent_t, hipEvent_t> et, ep;
+  const bool ot = t && take_events(et), op = p && take_events(ep);
+  if (ot) (void)hipEventRecord(et.first, s);
+  if (op) (void)hipEventRecord(ep.first, s);
   const int rc = launch();
-  (void)hipEventRecord(ev.second, s);
-  g_timing.used.push_back({ev.first, ev.second, id});
+  if (op) (void)hipEventRecord(ep.second, s);
+  if (ot) (void)hipEventRecord(et.second, s);
+  if (ot) g_timing.used.push_back({et.first, et.second, id});
+  if (op) {
+    g_prof.pending.push_back({ep.first, ep.second, id});
+    if (g_prof.pending.size() >= 2048) (void)prof_fold(1024);
+  }
   return rc;
 }
 
@@ -162,6 +216,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 
 struct Ws {
   size_t dmax = 0, rflag = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
+         gocc_b = 0, grgb_b = 0,  // fused mapper loss: d raw of a backward that is not d loss alone
          coef_d = 0, coef_c = 0, bslab = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
          dtemp_bytes = 0,
          total = 0;
@@ -223,7 +278,7 @@ static bool stage_fuse(const Plan& pl, const nc_grid* grids) {
 }
 
 void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1,
-            bool jac = false, bool claims = false, bool fuse = false) {
+            bool jac = false, bool claims = false, bool fuse = false, bool fused_loss = false) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -253,6 +308,11 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
   if (loss) {  // per-ray loss derivatives, forward -> backward
     w.coef_d = take((size_t)N * 8);
     w.coef_c = take((size_t)N * 12);
+  }
+  if (fused_loss) {  // k_composite_fwd_loss's d raw (d loss = 1) stays in gocc / grgb for every
+                     // loss-only backward of a retained graph; any other backward writes here
+    w.gocc_b = take((size_t)P * 4);
+    w.grgb_b = take((size_t)P * 12);
   }
   w.save = save;
   // the fused gather (k_mlp_fwd) cannot claim sparse rows or save the Jacobian
@@ -484,7 +544,8 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
   layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w, vbits,
-         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids), stage_fuse(pl, a->grids));
+         (a->flags & NC_SAVE_POINT_JACOBIAN) != 0, stage_claims(pl, a->grids), stage_fuse(pl, a->grids),
+         fused_mapper_loss(a));
   if (w.det && w.dtemp_bytes == 0) return fail(-1, "nicecore: radix-sort scratch size query failed");
   return 0;
 }
@@ -661,6 +722,35 @@ int nc_timing_stop(double* total_ms, int64_t* launches, int max_kernels) {
 
 const char* nc_kernel_name(int id) { return (id >= 0 && id < KID_COUNT) ? kKernelNames[id] : ""; }
 
+int nc_profile_report(void) {
+  if (!profile_on()) return 0;
+  const int rc = prof_fold(g_prof.pending.size());
+  int order[KID_COUNT];
+  int n = 0;
+  for (int k = 0; k < KID_COUNT; ++k)
+    if (g_prof.launches[k] > 0) order[n++] = k;
+  for (int a = 1; a < n; ++a)  // by total time, descending
+    for (int b = a; b > 0 && g_prof.total_ms[order[b]] > g_prof.total_ms[order[b - 1]]; --b) {
+      const int x = order[b];
+      order[b] = order[b - 1];
+      order[b - 1] = x;
+    }
+  double all = 0.0;
+  for (int a = 0; a < n; ++a) all += g_prof.total_ms[order[a]];
+  std::fprintf(stderr, "[NICE_CORE_PROFILE] per-kernel HIP-event times (launch stream)\n");
+  std::fprintf(stderr, "  %-22s %10s %12s %10s %7s\n", "kernel", "launches", "total ms", "avg us", "share");
+  for (int a = 0; a < n; ++a) {
+    const int k = order[a];
+    std::fprintf(stderr, "  %-22s %10lld %12.3f %10.2f %6.1f%%\n", kKernelNames[k], (long long)g_prof.launches[k],
+                 g_prof.total_ms[k], 1e3 * g_prof.total_ms[k] / (double)g_prof.launches[k],
+                 all > 0.0 ? 100.0 * g_prof.total_ms[k] / all : 0.0);
+  }
+  if (g_prof.captured)
+    std::fprintf(stderr, "  (%lld launches enqueued during graph capture: replays not timed)\n",
+                 (long long)g_prof.captured);
+  return rc;
+}
+
 size_t nc_struct_size(int which) {
   switch (which) {
     case 0: return sizeof(nc_render_args);
@@ -768,10 +858,19 @@ int nc_render_backward(const nc_render_args* a, void* ws, size_t ws_bytes, void*
   if (!any) return 0;
   // a fused mapper loss whose only upstream gradient is d loss: the forward's
   // k_composite_fwd_loss already wrote d raw for d loss = 1, k_mlp_dx scales by d loss
-  if (fused_mapper_loss(a) && a->g_loss && !a->g_depth && !a->g_var && !a->g_color)
+  if (fused_mapper_loss(a) && a->g_loss && !a->g_depth && !a->g_var && !a->g_color) {
     m.dout_scale = a->g_loss;
-  else if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd"))
-    return e;
+  } else {
+    if (fused_mapper_loss(a)) {  // keep the forward's d raw for d loss = 1 (a retained graph's next
+                                 // loss-only backward reads it): this backward's d raw goes elsewhere
+      rc.gocc = at<float>(ws, w.gocc_b);
+      rc.grgb = at<float>(ws, w.grgb_b);
+      m.gocc = rc.gocc;
+      m.grgb = rc.grgb;
+    }
+    if (int e = check_hip(timed(KID_COMPOSITE_BWD, s, [&] { return launch_composite_bwd(rc, s); }), "k_composite_bwd"))
+      return e;
+  }
   const DetBufs det = det_bufs(ws, w);
   return mlp_backward(m, a->dec, P, s, &det, need_coord ? &rc : nullptr,  // (+ ray grads, fused)
                       (a->flags & NC_DEFER_PARAM_GRADS) != 0);

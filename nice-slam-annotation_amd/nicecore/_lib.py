@@ -171,6 +171,7 @@ EXPORTS = {
     "nc_render_backward_params": (c_int, [POINTER(NcRenderArgs), c_void_p, c_size_t, c_void_p]),
     "nc_timing_start": (c_int, [ctypes.c_uint32]),
     "nc_timing_stop": (c_int, [POINTER(c_double), POINTER(c_int64), c_int]),
+    "nc_profile_report": (c_int, []),
     "nc_kernel_name": (ctypes.c_char_p, [c_int]),
     "nc_points_workspace_bytes": (c_size_t, [POINTER(NcPointsArgs)]),
     "nc_points_forward": (c_int, [POINTER(NcPointsArgs), c_void_p, c_size_t, c_void_p]),
@@ -221,6 +222,9 @@ def load(path: str | None = None):
     if lib.nc_abi_version() != NC_ABI_VERSION:
         raise NiceCoreError("libnicecore.so ABI version mismatch; rebuild it")
     _lib = lib
+    if os.environ.get("NICE_CORE_PROFILE") == "1":  # per-kernel timings at exit
+        import atexit
+        atexit.register(lib.nc_profile_report)
     return lib
 
 

@@ -197,3 +197,20 @@ def test_imap_param_count_matches_module(lib):
     """nc_imap_param_count == the iMAP* MLP's parameter count (config.py:28-32)."""
     m = D.build_imap(seed=0)
     assert lib.nc_imap_param_count() == sum(p.numel() for p in m.parameters()) == 222747
+
+
+def test_host_abi_under_address_sanitizer():
+    """the host side of the ABI (argument validation, stage plans, workspace
+    layouts of every entry point over the BASELINE shapes, malformed calls) built with
+    -Xarch_host -fsanitize=address,undefined (tools/asan/build.py) and run without a GPU:
+    no sanitizer report, every documented result holds."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("nicecore_asan_build", os.path.join(REPO, "tools", "asan", "build.py"))
+    asan_build = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(asan_build)
+    exe = asan_build.build()
+    r = asan_build.run(exe)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out, out[-4000:]
+    assert "abi_host_check: ok" in out

@@ -212,6 +212,27 @@ def test_fused_loss_with_output_gradients():
 
 
 @pytest.mark.gpu
+def test_fused_loss_retain_graph_second_backward():
+    """A backward with output gradients runs k_composite_bwd (d raw of loss + depth terms);
+    on a retained graph a later backward of the loss alone takes the fused path again and
+    must still find the forward's d raw for d loss = 1 (not the first backward's): it equals
+    the loss-only backward of a fresh render."""
+    rec, stage, model, g, ro, rd, r = _setup("color_depth")
+    gt, gtc = rec["gt_depth"].cuda(), rec["gt_color"].cuda()
+    d1, v1, c1, L1 = r.render_batch_loss(g, model, rd, ro, "cuda", stage, gt, gtc, loss="mapper", color_term=True)
+    (L1 + 0.5 * d1.sum() + (c1 * c1).sum()).backward(retain_graph=True)
+    _grads(model, g, ro, rd)
+    L1.backward()
+    G1 = _grads(model, g, ro, rd)
+    L2 = r.render_batch_loss(g, model, rd, ro, "cuda", stage, gt, gtc, loss="mapper", color_term=True)[3]
+    L2.backward()
+    G2 = _grads(model, g, ro, rd)
+    assert set(G1) == set(G2)
+    bad = {k: rel_err(G1[k].cpu(), G2[k].cpu()) for k in G1 if rel_err(G1[k].cpu(), G2[k].cpu()) > 1e-6}
+    assert not bad, bad
+
+
+@pytest.mark.gpu
 def test_no_weight_grad_flag_is_enforced(monkeypatch):
     """NC_NO_WEIGHT_GRAD(kind) (include/nicecore.h) spares the forward's activation records
     of a decoder; a backward that then asks for that decoder's weight gradient must fail
