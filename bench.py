@@ -45,6 +45,9 @@ SPLIT16_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 MFMA_PEAK = {"k_mlp_fwd": SPLIT16_PEAK_TFLOPS, "k_mlp_dx": FP32_MFMA_PEAK_TFLOPS, "k_mlp_dw": FP32_MFMA_PEAK_TFLOPS,
              "k_grid_gather": FP32_MFMA_PEAK_TFLOPS}
 HBM_PEAK_GBS = 8000.0
+# MI355X_MICROARCH.md "Global float atomics": no-return f32 atomics execute at the memory side,
+# chip-wide ~1.3 TB/s of added bytes (1.26-1.36) whatever the contention pattern
+ATOMIC_PEAK_GBS = 1300.0
 MAC = {"coarse": 6176, "middle": 15479, "fine": 20599, "color": 15575}  # per point
 TRI_FLOP = 8 * 32 * 2  # one trilinear lookup of 32 channels
 # dX-chain MACs per point: the fine decoder's fc_c input gradient is only taken for its
@@ -98,6 +101,14 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="time the eager step instead of its hipGraph replay "
                          "(nicecore.graph.GraphedStep)")
+    ap.add_argument("--global-batch", action="store_true",
+                    help="draw ONE batch of N x --rays rays (seed 1000) and give rank r its contiguous shard "
+                         "(distributed.shard), instead of --rays fresh rays per rank: the N-rank step then "
+                         "computes the gradients of the 1-rank step over the whole batch (tests)")
+    ap.add_argument("--dump-grads", default=None,
+                    help="after the timed steps run one more step and have rank 0 save its exchanged "
+                         "gradients (decoder parameters; grid rows of the frustum, or whole grids without "
+                         "one) with torch.save to this path (tests/test_gpu_bench_ranks.py)")
     return ap.parse_args()
 
 
@@ -195,7 +206,11 @@ def build_workload(args, rank, device, world=1):
     for n in ("middle", "fine", "color"):
         getattr(model, n + "_decoder").bound = model.bound
     model.coarse_decoder.bound = (sc.bound * 2).to(device)
-    ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000 + rank)
+    if getattr(args, "global_batch", False):  # one batch over all ranks, contiguous shards
+        from nicecore.distributed import shard
+        ro, rd, dep, col = shard(rank, world, *S.synth_rays(sc, args.rays * world, seed=1000))
+    else:
+        ro, rd, dep, col = S.synth_rays(sc, args.rays, seed=1000 + rank)
     slam = types.SimpleNamespace(nice=True, bound=sc.bound, H=sc.H, W=sc.W, fx=sc.fx, fy=sc.fy,
                                  cx=sc.cx, cy=sc.cy)
     cfg = {"rendering": dict(S.DEFAULT_RENDERING, param_grads=getattr(args, "param_grads", "direct")), "scale": 1, "occupancy": True}
@@ -612,14 +627,22 @@ def main():
         gbs = by / t / 1e9
         mpeak = MFMA_PEAK.get(dominant, FP32_MFMA_PEAK_TFLOPS)
         ridge = mpeak * 1e12 / (HBM_PEAK_GBS * 1e9)  # FLOP per byte
-        hbm_bound = by > 0 and fl / by < ridge
         tr = read_traffic(args)
-        traffic = ((tr or {}).get("kernels", {}).get(dominant) or {}).get("hbm_bytes")
-        roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dominant,
-                "achieved": round(gbs if hbm_bound else tflops, 3),
-                "peak": HBM_PEAK_GBS if hbm_bound else mpeak,
-                "unit": "GB/s" if hbm_bound else "TFLOP/s",
-                "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / mpeak, 4),
+        kt_pmc = (tr or {}).get("kernels", {}).get(dominant) or {}
+        traffic = kt_pmc.get("hbm_bytes")
+        atomic = kt_pmc.get("atomic_bytes")  # PMC TCC_EA0_ATOMIC x 64 B, same workload
+        # the limiter = the highest of the fractions: HBM (SURVEY §8(d) bytes), MFMA (algorithmic
+        # FLOP) and, where the PMC summary has it, the memory-side float-atomic path
+        fracs = {"hbm": gbs / HBM_PEAK_GBS, "mfma": tflops / mpeak}
+        if atomic:
+            fracs["atomic"] = atomic / t / 1e9 / ATOMIC_PEAK_GBS
+        bound = max(fracs, key=fracs.get)
+        ach = {"hbm": gbs, "mfma": tflops, "atomic": (atomic or 0) / t / 1e9}[bound]
+        roof = {"bound": bound, "kernel": dominant,
+                "achieved": round(ach, 3),
+                "peak": {"hbm": HBM_PEAK_GBS, "mfma": mpeak, "atomic": ATOMIC_PEAK_GBS}[bound],
+                "unit": "TFLOP/s" if bound == "mfma" else "GB/s",
+                "frac": round(fracs[bound], 4),
                 "traffic": traffic,
                 "traffic_source": (tr or {}).get("source"),
                 "traffic_frac": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
@@ -635,6 +658,9 @@ def main():
                 "mfma_tflops": round(tflops, 3), "mfma_peak_tflops": round(mpeak, 1),
                 "mfma_frac": round(tflops / mpeak, 4),
                 "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                "atomic_bytes": atomic, "atomic_gbs": round(atomic / t / 1e9, 1) if atomic else None,
+                "atomic_peak_gbs": ATOMIC_PEAK_GBS,
+                "atomic_frac": round(fracs["atomic"], 4) if atomic else None,
                 "timing": timing_src}
     peak_rays, f_ray, b_ray = step_roofline_rays_s(args.stage, S, args.mode, args.fix_fine)
 
@@ -670,6 +696,22 @@ def main():
         f"eager_{other}_ms_per_step": round(eager_other_ms, 4),
         "kernels_ms": {k: round(v, 4) for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1])},
     }
+    if args.dump_grads:
+        eager()  # one more step: render + loss + backward + the gradient exchange
+        torch.cuda.synchronize()
+        if rank == 0:
+            dump = {"world": world, "rays_per_rank": args.rays,
+                    "params": {n: p.grad.detach().cpu() for n, p in w["model"].named_parameters()
+                               if p.grad is not None}, "grids": {}}
+            for k, g in w["grids"].items():
+                if g.grad is None:
+                    continue
+                flat = g.grad.detach()[0].reshape(g.shape[1], -1)  # [C, D*H*W]
+                rows = (w["frustum"] or {}).get(k)
+                dump["grids"][k] = (flat[:, rows] if rows is not None else flat).cpu()
+            if w["frustum"] is not None:
+                dump["frustum_rows"] = {k: v.cpu() for k, v in w["frustum"].items()}
+            torch.save(dump, args.dump_grads)
     if args.iteration and world == 1 and w["ba"] and w["sparse"] is None:
         out["mapper_iteration_ms"] = time_mapper_iteration(w, args)
     if world == 1 and rank == 0 and args.cpu_seconds > 0:

@@ -6,7 +6,9 @@ A masked render of N rays must equal rendering the compacted batch rays[mask]:
   * kept rays' depth / uncertainty / colour and ray gradients bit-identical (every point's
     decoder chains and every ray's compositing are independent of the other rays; the
     batch-global max(gt_depth) is taken over the kept rays, Renderer.py:157, :194);
-  * the loss (mapper, tracker with handle_dynamic's median over the kept rays) to 1e-12;
+  * the loss (mapper, tracker with handle_dynamic's median over the kept rays): the float64
+    depth term to 1e-12; with the float32 colour term to 1e-6 relative (its per-workgroup
+    partial sums group the rays differently in the two batches; tests/test_gpu_loss.py);
   * grid and decoder-parameter gradients to 1e-6 of max-abs (float atomics / a different
     point blocking of the weight-gradient sums);
   * dropped rays: outputs and ray gradients exactly 0.
@@ -94,7 +96,7 @@ def test_masked_equals_compacted(mode, fused):
     for k in ("depth", "var", "color"):
         assert torch.equal(om[k][keep], oc[k]), k
         assert not bool(om[k][~keep].any()), k  # dropped rays report 0
-    assert abs(lm - lc) <= 1e-12 * max(abs(lc), 1.0), (lm, lc)
+    assert abs(lm - lc) <= 1e-6 * max(abs(lc), 1.0), (lm, lc)  # colour term on: test_gpu_loss.py's bound
     for k in ("grad/rays_o", "grad/rays_d"):
         assert torch.equal(gm[k][keep], gc[k]), k
         assert not bool(gm[k][~keep].any()), k
@@ -156,7 +158,7 @@ def test_non_finite_dropped_rays_stay_out():
     rd[bad[3], 0] = 0.0
     om, lm, gm = _run(sc, grids, params, ro, rd, dep, col, keep, "ba", True)
     oc, lc, gc = _run(sc, grids, params, ro[keep], rd[keep], dep[keep], col[keep], None, "ba", True)
-    assert abs(lm - lc) <= 1e-12 * max(abs(lc), 1.0)
+    assert abs(lm - lc) <= 1e-6 * max(abs(lc), 1.0)
     for k in ("depth", "var", "color"):
         assert torch.equal(om[k][keep], oc[k]), k
     for k in gm:
@@ -175,7 +177,8 @@ def test_masked_step_graph_replay_follows_the_mask():
     r = make_renderer(sc.bound)
     gt, gtc = dep.cuda(), col.cuda()
     mask = keep.cuda().clone()
-    leaves = list(g.values()) + list(model.parameters()) + [ro_g, rd_g]
+    leaves = [g[k] for k in ("grid_middle", "grid_fine", "grid_color")] + \
+        [p for n, p in model.named_parameters() if not n.startswith("coarse_decoder.")] + [ro_g, rd_g]
     out = {}
 
     def body():
@@ -198,6 +201,6 @@ def test_masked_step_graph_replay_follows_the_mask():
         mask.copy_(mk.cuda())
         loss = step()
         torch.cuda.synchronize()
-        assert abs(float(loss) - l0) <= 1e-12 * max(abs(l0), 1.0)
+        assert abs(float(loss) - l0) <= 1e-6 * max(abs(l0), 1.0)
         for t, gr in zip(leaves, g0):
             assert rel_err(t.grad.cpu(), gr.cpu()) <= 1e-6

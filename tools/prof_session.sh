@@ -23,4 +23,6 @@ run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o 
     python3 "$ROOT/bench.py" "$@" --cpu-seconds 0 &&
 run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- \
     python3 "$ROOT/bench.py" "$@" --cpu-seconds 0 &&
-python3 "$ROOT/tools/pmc_traffic.py" "$out/fetch" "$out/write" "$out/hbm_traffic.json" "$@"
+run atomic 300 rocprofv3 --pmc TCC_EA0_ATOMIC_sum --output-format csv -d "$out/atomic" -o run -- \
+    python3 "$ROOT/bench.py" "$@" --cpu-seconds 0 &&
+python3 "$ROOT/tools/pmc_traffic.py" --atomic "$out/atomic" "$out/fetch" "$out/write" "$out/hbm_traffic.json" "$@"
