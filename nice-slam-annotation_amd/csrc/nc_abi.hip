@@ -177,6 +177,15 @@ int check_grid(const nc_grid& g, const char* name) {
   if (!g.data) return fail(-1, std::string("nicecore: grid ") + name + " is required by this stage but NULL");
   for (int k = 0; k < 3; ++k)
     if (g.dims[k] < 1) return fail(-1, std::string("nicecore: grid ") + name + " has an empty dimension");
+  // the kernels index voxels in int32 and take element strides as int32 (nc_device.h Corners)
+  for (int k = 0; k < 3; ++k)
+    if (g.dims[k] > (INT32_MAX >> 1)) return fail(-1, std::string("nicecore: grid ") + name + " dimension >= 2^30");
+  for (int k = 0; k < 4; ++k) {
+    if (g.stride[k] < 0 || g.stride[k] > INT32_MAX)
+      return fail(-1, std::string("nicecore: grid ") + name + " has an element stride outside [0, 2^31)");
+    if (g.grad && !g.grad_rows && (g.grad_stride[k] < 0 || g.grad_stride[k] > INT32_MAX))
+      return fail(-1, std::string("nicecore: grid ") + name + " gradient has an element stride outside [0, 2^31)");
+  }
   if (g.grad_rows) {  // sparse gradient rows (ABI v5)
     if (!g.row_voxel || !g.row_count || g.row_capacity < 1 || !g.grad ||
         (reinterpret_cast<uintptr_t>(g.grad) & 15))

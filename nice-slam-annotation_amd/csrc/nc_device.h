@@ -227,14 +227,49 @@ struct NetH {
 // bit2 = z).  Compiled with -ffp-contract=off, so the forward value is
 // bit-identical to the CPU reference.
 // ---------------------------------------------------------------------------
+// Index arithmetic: the clip keeps ix in [0, W-1] (NaN clips to W-1), so the corner-0
+// voxel indices are non-negative int32 and corner k is outside the grid only on the far
+// side (x0 + 1 == W, ...).  Element strides are int32 (the host rejects a grid whose
+// strides reach 2^31: check_grid); the corner-0 offset is one 64-bit value (the C5 grids
+// hold 6.5G elements) and corner k adds the wave-uniform stride sum of its sides.
 struct Corners {
-  int64_t off[8];  // element offset of the corner (channel 0) in the grid
+  int64_t base;    // element offset of corner 0 (channel 0) in the grid
   float w[8];      // interpolation weight (0 where the corner is out of bounds)
   float wx[2], wy[2], wz[2];  // per-axis factors [west/east], [north/south], [top/bottom]
   float gmx, gmy, gmz;        // d(ix)/d(x_norm) incl. border-clip gradient
   unsigned inb;                // bit k: corner k inside the grid
-  int64_t x0, y0, z0;          // corner 0 (tnw) voxel coordinates
+  int32_t x0, y0, z0;          // corner 0 (tnw) voxel coordinates
 };
+
+// element strides of a grid (or its gradient) as int32 (check_grid / check_grad_strides)
+__device__ __forceinline__ int32_t stride32(const int64_t s) { return (int32_t)s; }
+
+// offset of corner k from corner 0 along the given strides (wave-uniform)
+__device__ __forceinline__ int64_t corner_delta(const int64_t (&st)[4], int k) {
+  return (int64_t)((k & 1) ? stride32(st[3]) : 0) + (int64_t)(((k >> 1) & 1) ? stride32(st[2]) : 0) +
+         (int64_t)((k >> 2) ? stride32(st[1]) : 0);
+}
+
+// element offset of corner k (0 for an out-of-bounds corner: it reads cell 0 instead)
+__device__ __forceinline__ int64_t corner_off(const nc_grid& G, const Corners& c, int k) {
+  return ((c.inb >> k) & 1u) ? c.base + corner_delta(G.stride, k) : (int64_t)0;
+}
+
+// 32 zero floats of each code object: a channels-last gather reads an out-of-bounds
+// corner from here, so its term v * w is exactly 0 without a select per channel (corner 0
+// is always inside, so the sum of the inside corners is unchanged)
+static __device__ __attribute__((aligned(16))) float kZeroRow[32];  // global (not constant) address space: the
+                                                                  // corner select stays a global_load, not a flat_load
+
+// channels-last corner row k of grid G (the zero row for an out-of-bounds corner)
+__device__ __forceinline__ const float* corner_row(const nc_grid& G, const Corners& c, int k) {
+  return ((c.inb >> k) & 1u) ? G.data + (c.base + corner_delta(G.stride, k)) : kZeroRow;
+}
+
+// element offset of voxel (x, y, z) along strides st
+__device__ __forceinline__ int64_t voxel_off(const int64_t (&st)[4], int32_t x, int32_t y, int32_t z) {
+  return (int64_t)z * stride32(st[1]) + (int64_t)y * stride32(st[2]) + (int64_t)x * stride32(st[3]);
+}
 
 __device__ __forceinline__ float clip_fwd(float v, float hi) {
   float t = (v < 0.f) ? 0.f : v;       // std::max(in, 0)
@@ -242,7 +277,7 @@ __device__ __forceinline__ float clip_fwd(float v, float hi) {
 }
 
 __device__ __forceinline__ void make_corners(const nc_grid& G, const float xyz[3], Corners& c) {
-  const int64_t D = G.dims[0], H = G.dims[1], W = G.dims[2];
+  const int32_t D = (int32_t)G.dims[0], H = (int32_t)G.dims[1], W = (int32_t)G.dims[2];
   const float sx = (float)(W - 1), sy = (float)(H - 1), sz = (float)(D - 1);
   float ix = ((xyz[0] + 1.f) / 2.f) * sx;
   float iy = ((xyz[1] + 1.f) / 2.f) * sy;
@@ -254,21 +289,22 @@ __device__ __forceinline__ void make_corners(const nc_grid& G, const float xyz[3
   ix = clip_fwd(ix, sx);
   iy = clip_fwd(iy, sy);
   iz = clip_fwd(iz, sz);
-  const int64_t x0 = (int64_t)floorf(ix), y0 = (int64_t)floorf(iy), z0 = (int64_t)floorf(iz);
+  const int32_t x0 = (int32_t)floorf(ix), y0 = (int32_t)floorf(iy), z0 = (int32_t)floorf(iz);
   c.x0 = x0; c.y0 = y0; c.z0 = z0;
   const float fx0 = (float)x0, fy0 = (float)y0, fz0 = (float)z0;
   const float fx1 = (float)(x0 + 1), fy1 = (float)(y0 + 1), fz1 = (float)(z0 + 1);
   c.wx[0] = fx1 - ix; c.wx[1] = ix - fx0;
   c.wy[0] = fy1 - iy; c.wy[1] = iy - fy0;
   c.wz[0] = fz1 - iz; c.wz[1] = iz - fz0;
-  c.inb = 0;
+  // corner k is inside unless one of its far sides leaves the grid (x0, y0, z0 >= 0 always)
+  const unsigned xo = (x0 + 1 < W) ? 0xffu : 0x55u;  // bit k kept where k's x side is 0 or x0 + 1 < W
+  const unsigned yo = (y0 + 1 < H) ? 0xffu : 0x33u;
+  const unsigned zo = (z0 + 1 < D) ? 0xffu : 0x0fu;
+  c.inb = xo & yo & zo;
+  c.base = voxel_off(G.stride, x0, y0, z0);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int xb = k & 1, yb = (k >> 1) & 1, zb = k >> 2;
-    const int64_t xx = x0 + xb, yy = y0 + yb, zz = z0 + zb;
-    const bool in = (xx >= 0 && xx < W && yy >= 0 && yy < H && zz >= 0 && zz < D);
-    c.inb |= (in ? 1u : 0u) << k;
-    c.off[k] = in ? (zz * G.stride[1] + yy * G.stride[2] + xx * G.stride[3]) : 0;
     c.w[k] = (c.wx[xb] * c.wy[yb]) * c.wz[zb];
   }
 }
@@ -291,7 +327,8 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
   float v[8][8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float* base = G.data + c.off[k];  // off = 0 for out-of-bounds corners
+    // VEC: out-of-bounds corners read the zero row; else cell 0, and the sum skips them
+    const float* base = VEC ? corner_row(G, c, k) : G.data + corner_off(G, c, k);
     if (VEC) {
       const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
       const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
@@ -305,7 +342,7 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const bool in = (c.inb >> k) & 1u;
+    const bool in = VEC || ((c.inb >> k) & 1u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[k][j] * c.w[k] : 0.f);
   }
@@ -323,7 +360,7 @@ __device__ __forceinline__ void gather8x2(const nc_grid& G1, const Corners& c1, 
     const Corners& c = q == 0 ? c1 : c2;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float* base = G.data + c.off[k];  // off = 0 for out-of-bounds corners
+      const float* base = corner_row(G, c, k);  // the zero row for out-of-bounds corners
       const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
       const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
       v[q][k][0] = a.x; v[q][k][1] = a.y; v[q][k][2] = a.z; v[q][k][3] = a.w;
@@ -338,9 +375,8 @@ __device__ __forceinline__ void gather8x2(const nc_grid& G1, const Corners& c1, 
     for (int j = 0; j < 8; ++j) out[j] = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const bool in = (c.inb >> k) & 1u;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[q][k][j] * c.w[k] : 0.f);
+      for (int j = 0; j < 8; ++j) out[j] = out[j] + v[q][k][j] * c.w[k];  // 0 * w from the zero row
     }
   }
 }
@@ -357,10 +393,7 @@ __device__ __forceinline__ void gather8_b2(const nc_grid& G, const Corners& c, i
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int k = 4 * h + kk;
-      const bool in = (c.inb >> k) & 1u;
-      const int64_t o = (c.z0 + (k >> 2)) * G.stride[1] + (c.y0 + ((k >> 1) & 1)) * G.stride[2] +
-                        (c.x0 + (k & 1)) * G.stride[3];
-      const float* base = G.data + (in ? o : 0);
+      const float* base = corner_row(G, c, k);  // the zero row for out-of-bounds corners
       const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
       const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
       v[kk][0] = a.x; v[kk][1] = a.y; v[kk][2] = a.z; v[kk][3] = a.w;
@@ -369,9 +402,8 @@ __device__ __forceinline__ void gather8_b2(const nc_grid& G, const Corners& c, i
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int k = 4 * h + kk;
-      const bool in = (c.inb >> k) & 1u;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[kk][j] * c.w[k] : 0.f);
+      for (int j = 0; j < 8; ++j) out[j] = out[j] + v[kk][j] * c.w[k];  // 0 * w from the zero row
     }
   }
 }

@@ -24,13 +24,10 @@ __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners&
     float v[4][8];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      // corner offset from the corner-0 voxel (not Corners::off: 16 fewer live VGPRs
-      // across the decoder backward); out-of-bounds corners read cell 0
+      // out-of-bounds corners read cell 0
       const int k = 4 * h + kk;
-      const bool in = (c.inb >> k) & 1u;
-      const int64_t o = (c.z0 + (k >> 2)) * G.stride[1] + (c.y0 + ((k >> 1) & 1)) * G.stride[2] +
-                        (c.x0 + (k & 1)) * G.stride[3];
-      const float* base = G.data + (in ? o : 0);
+      // VEC: out-of-bounds corners read the zero row (their dot is 0); else cell 0, skipped below
+      const float* base = VEC ? corner_row(G, c, k) : G.data + corner_off(G, c, k);
       if (VEC) {
         const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
         const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
@@ -41,10 +38,11 @@ __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners&
         for (int j = 0; j < 8; ++j) v[kk][j] = base[(int64_t)feat_of(j, g) * sC];
       }
     }
+    __builtin_amdgcn_sched_barrier(0);  // the batch's loads all issue before the first is consumed
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int k = 4 * h + kk;
-      if (!((c.inb >> k) & 1u)) continue;  // out-of-bounds corner: no contribution
+      if (!VEC && !((c.inb >> k) & 1u)) continue;  // out-of-bounds corner: no contribution
       const int xb = k & 1, yb = (k >> 1) & 1, zb = k >> 2;
       float dot = 0.f;
 #pragma unroll
@@ -93,20 +91,20 @@ __device__ __forceinline__ void grid_scatter_stage(const nc_grid& G, const Corne
     Wt[(2 * g) * SCAT_KLD + i] = (c.wx[0] * wy) * wz;
     Wt[(2 * g + 1) * SCAT_KLD + i] = (c.wx[1] * wy) * wz;
     if (G.grad_rows) {  // sparse gradient rows: the rows the forward claimed (-1: none, skipped)
-      const int64_t v = ((c.z0 + zb) * G.dims[1] + (c.y0 + yb)) * G.dims[2] + c.x0;
+      const int64_t v = ((int64_t)(c.z0 + zb) * G.dims[1] + (c.y0 + yb)) * G.dims[2] + c.x0;
       const int k0 = 2 * g, k1 = 2 * g + 1;
       const int r0 = ((c.inb >> k0) & 1u) ? G.grad_rows[v] : -1;
       const int r1 = ((c.inb >> k1) & 1u) ? G.grad_rows[v + 1] : -1;
       OFF[k0 * SCAT_KLD + i] = r0 < 0 ? -1 : (int64_t)r0 * 32;
       OFF[k1 * SCAT_KLD + i] = r1 < 0 ? -1 : (int64_t)r1 * 32;
     } else {
-      const int64_t base = (c.z0 + zb) * G.grad_stride[1] + (c.y0 + yb) * G.grad_stride[2] + c.x0 * G.grad_stride[3];
+      const int64_t base = voxel_off(G.grad_stride, c.x0, c.y0 + yb, c.z0 + zb);
       OFF[(2 * g) * SCAT_KLD + i] = base;
-      OFF[(2 * g + 1) * SCAT_KLD + i] = base + G.grad_stride[3];
+      OFF[(2 * g + 1) * SCAT_KLD + i] = base + stride32(G.grad_stride[3]);
     }
   }
   if (g == 0) {
-    KEY[i] = valid ? (c.x0 | (c.y0 << 21) | (c.z0 << 42)) : -1;
+    KEY[i] = valid ? ((int64_t)c.x0 | ((int64_t)c.y0 << 21) | ((int64_t)c.z0 << 42)) : -1;
     INB[i] = valid ? (int)c.inb : 0;
   }
 }
@@ -120,7 +118,7 @@ __device__ __forceinline__ void grid_scatter_flush(const nc_grid& G, const float
   const int64_t* KEY = reinterpret_cast<const int64_t*>(reg + SCAT_KEY);
   const int* INB = reinterpret_cast<const int*>(reg + SCAT_INB);
   const int half = lane >> 5, ch = lane & 31;
-  const int64_t chs = G.grad_rows ? (int64_t)ch : (int64_t)ch * G.grad_stride[0];
+  const int64_t chs = G.grad_rows ? (int64_t)ch : (int64_t)ch * stride32(G.grad_stride[0]);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   auto flush = [&](int pt, int xb, int q, float v) {
     const int k = xb | (q << 1);

@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256) k_grid_gather(const MlpCtx ctx) {
   for (int k = 0; k < 8; ++k) {
 #pragma unroll
     for (int h = 0; h < GATHER_V4; ++h) {
-      const float* base = G.data + co.off[k] + (vec ? c0 + 4 * h : (c0 + 4 * h) * sC);
+      const float* base = G.data + corner_off(G, co, k) + (vec ? c0 + 4 * h : (c0 + 4 * h) * sC);
       if (vec) {
         v[k][h] = *reinterpret_cast<const float4*>(base);
       } else {

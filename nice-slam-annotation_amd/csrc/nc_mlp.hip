@@ -1055,6 +1055,13 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
           const float gk = sum_groups(gi[k]) * gm[k];
           gg[k] = ((double)gk * 2.0) / (D.bound[k][1] - D.bound[k][0]);
         }
+        // the point gradient leaves before the scatter (its registers are free across the
+        // scatter walk's loop)
+        if (valid && g == 0) {
+          double* dst = ctx.dpts + ((int64_t)job.slot * ctx.P + p) * 3;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) dst[k] = gg[k] + (double)dpf[k];
+        }
       }
 #ifndef NC_ABL_DX_NO_SCATTER  // timing-only ablation: no grid scatter
       if (need_grid) {
@@ -1069,11 +1076,6 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         }
       }
 #endif
-    }
-    if (need_coord && valid && g == 0) {
-      double* dst = ctx.dpts + ((int64_t)job.slot * ctx.P + p) * 3;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dst[k] = gg[k] + (double)dpf[k];
     }
   }
   if constexpr (N::XYZ) {  // this workgroup's d B partial -> its bslab row (k_mlp_dw folds the rows into its slab)

@@ -568,7 +568,7 @@ class NiceRenderFn(torch.autograd.Function):
             rv = rv.detach().reshape(-1)
             if rv.shape[0] != N or rv.device != device:
                 raise L.NiceCoreError("ray_mask must hold one entry per ray, on the render device")
-            rv = rv.to(torch.uint8).contiguous()
+            rv = (rv.view(torch.uint8) if rv.dtype == torch.bool else rv.to(torch.uint8)).contiguous()
             a.ray_valid = rv.data_ptr()
         grids = (g0, g1, g2, g3)
         gkeep = []

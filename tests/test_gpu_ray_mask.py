@@ -179,7 +179,6 @@ def test_masked_step_graph_replay_follows_the_mask():
     mask = keep.cuda().clone()
     leaves = [g[k] for k in ("grid_middle", "grid_fine", "grid_color")] + \
         [p for n, p in model.named_parameters() if not n.startswith("coarse_decoder.")] + [ro_g, rd_g]
-    out = {}
 
     def body():
         for t in leaves:
@@ -187,15 +186,14 @@ def test_masked_step_graph_replay_follows_the_mask():
         d, u, c, loss = r.render_batch_loss(g, model, rd_g, ro_g, "cuda", "color", gt, gtc, loss="mapper",
                                             w_color_loss=0.2, color_term=True, ray_mask=mask)
         loss.backward()
-        out["loss"] = loss
-        return loss
+        return loss.detach()
 
     masks = [keep, torch.roll(keep, 7), torch.ones_like(keep)]
     eager = []
     for mk in masks:
         mask.copy_(mk.cuda())
-        body()
-        eager.append((float(out["loss"]), [t.grad.detach().clone() for t in leaves]))
+        lv = body()
+        eager.append((float(lv), [t.grad.detach().clone() for t in leaves]))
     step = GraphedStep(body)
     for (l0, g0), mk in zip(eager, masks):
         mask.copy_(mk.cuda())

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 4 session d: int32 corner indexing + zero-row out-of-bounds corners + dx corner batches:
+# A/B against the round's base library on one box, ray-mask tests, GPU suite
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out/r4d
+mkdir -p $O
+step() { # name seconds cmd...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "[$n] rc=$rc"; tail -6 $O/$n.log | cut -c1-1500
+  if [ $rc -ge 124 ]; then exit $rc; fi
+}
+step ab 600 python3 -u tools/ablate.py run r4base r4cur r4base r4cur
+step mask 300 python3 -u -m pytest tests/test_gpu_ray_mask.py -m gpu -v --timeout 200 --timeout-method thread
+step tests_all 1000 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
