@@ -226,6 +226,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 struct Ws {
   size_t dmax = 0, rflag = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
          gocc_b = 0, grgb_b = 0,  // fused mapper loss: d raw of a backward that is not d loss alone
+         lpart = 0, lcount = 0,   // fused mapper loss: per-workgroup partial sums + done counter
          coef_d = 0, coef_c = 0, bslab = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
          dtemp_bytes = 0,
          total = 0;
@@ -322,6 +323,8 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
                      // loss-only backward of a retained graph; any other backward writes here
     w.gocc_b = take((size_t)P * 4);
     w.grgb_b = take((size_t)P * 12);
+    w.lpart = take((size_t)fused_loss_blocks(N) * 16);
+    w.lcount = take(16);
   }
   w.save = save;
   // the fused gather (k_mlp_fwd) cannot claim sparse rows or save the Jacobian
@@ -508,7 +511,8 @@ int gather_and_claim(MlpCtx& m, const Ws& w, hipStream_t s) {
 
 // NC_LOSS_MAPPER forward for a backward: compositing, loss terms and the compositing
 // backward for d loss = 1 in one kernel (k_composite_fwd_loss; NICECORE_FUSED_LOSS=0 for
-// the three-kernel path).  NC_DETERMINISTIC keeps k_loss's fixed-order loss sum.
+// the three-kernel path).  Both sum the loss in a fixed order; NC_DETERMINISTIC keeps the
+// three-kernel path (k_loss's value, the reference's expression order).
 bool fused_mapper_loss(const nc_render_args* a) {
   static int on = -1;
   if (on < 0) {
@@ -615,6 +619,10 @@ void fill_ray(RayCtx& c, const nc_render_args* a, const Plan& pl, void* ws, cons
     c.coef_c = at<float>(ws, w.coef_c);
   }
   c.valid = a->ray_valid;
+  if (w.lcount) {
+    c.loss_part = at<double>(ws, w.lpart);
+    c.loss_count = at<unsigned>(ws, w.lcount);
+  }
 }
 
 int fwd_grid_x(int64_t P, int n_jobs, int which) {

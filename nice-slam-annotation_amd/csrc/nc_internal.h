@@ -177,7 +177,12 @@ struct RayCtx {
   int32_t fuse_bwd;          // NC_LOSS_MAPPER forward for a backward: k_composite_fwd_loss writes the
                              // loss's d raw for d loss = 1 (gocc / grgb); no k_loss, no k_composite_bwd
   const uint8_t* valid;      // [N] nc_render_args.ray_valid (0 = ray dropped), or NULL
+  double* loss_part;         // fused loss: [fused_loss_blocks(N)][2] per-workgroup (depth, colour) sums
+  unsigned* loss_count;      // fused loss: workgroups done (zeroed by k_ray_setup; the last one sums)
 };
+
+// k_composite_fwd_loss workgroups for N rays (the length of RayCtx::loss_part)
+int64_t fused_loss_blocks(int64_t N);
 
 // ray r is kept (nc_render_args.ray_valid)
 __device__ __forceinline__ bool ray_ok(const RayCtx& c, int64_t r) { return c.valid == nullptr || c.valid[r] != 0; }

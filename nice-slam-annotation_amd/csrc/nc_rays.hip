@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x < MAX_JOBS && c.range_flag) c.range_flag[threadIdx.x] = 0u;  // for k_mlp_fwd
-  if (blockIdx.x == 0 && threadIdx.x == 0 && c.fuse_bwd) *c.loss_out = 0.0;  // k_composite_fwd_loss adds into it
+  if (blockIdx.x == 0 && threadIdx.x == 0 && c.fuse_bwd) *c.loss_count = 0u;  // k_composite_fwd_loss's done counter
   // this ray's inputs first: their loads overlap the batch-max loop below
   const bool live = r < c.N;
   const int64_t rr = live ? r : 0;
@@ -561,10 +561,11 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
 // NC_LOSS_MAPPER terms (the same expressions) and k_composite_bwd for d loss = 1;
 // k_mlp_dx multiplies by the actual d loss (MlpCtx::dout_scale), so the backward skips
 // k_composite_bwd (and the forward k_loss).  coef_d / coef_c are still written for a
-// backward that also receives depth / var / colour gradients.  The loss value: the
-// workgroup's 16 rays summed in wave order, one float64 atomic per workgroup into
-// loss_out (zeroed by k_ray_setup) -- the last bits depend on the workgroups' order;
-// NC_DETERMINISTIC keeps k_loss's fixed-order sum.
+// backward that also receives depth / var / colour gradients.  The loss value, in a
+// fixed order (run-to-run identical): each workgroup stores its rays' float64 depth and
+// colour sums to loss_part, and the last workgroup to finish (loss_count, zeroed by
+// k_ray_setup) sums the partials in block order and applies w_color once to the
+// float32-rounded colour total, as k_loss does (Mapper.py:609-612).
 // ---------------------------------------------------------------------------
 #ifndef NC_FUSED_RAYS
 #define NC_FUSED_RAYS 16
@@ -612,16 +613,47 @@ __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const Ra
     part[wv][1] = lc;
   }
   __syncthreads();
+  __shared__ int last;
   if (threadIdx.x == 0) {
     double d = 0.0, cs = 0.0;
     for (int w = 0; w < FUSED_RAYS; ++w) {
       d += part[w][0];
       cs += part[w][1];
     }
-    if (col_term) d = d + (double)(c.w_color * (float)cs);
-    atomicAdd(c.loss_out, d);
+    c.loss_part[2 * blockIdx.x] = d;
+    c.loss_part[2 * blockIdx.x + 1] = cs;
+    __threadfence();  // the partials are visible device-wide before the count says so
+    last = atomicAdd(c.loss_count, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // the last workgroup: every partial in block order (thread t: blocks t, t + 64 * FUSED_RAYS,
+  // ...), then the wave butterfly and the waves in order -- one association for any timing
+  double d = 0.0, cs = 0.0;
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += 64 * FUSED_RAYS) {
+    d += c.loss_part[2 * b];
+    cs += c.loss_part[2 * b + 1];
+  }
+  d = wsum_d(d);
+  cs = wsum_d(cs);
+  __syncthreads();  // part[][] is reused
+  if (lane == 0) {
+    part[wv][0] = d;
+    part[wv][1] = cs;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ds = 0.0, css = 0.0;
+    for (int w = 0; w < FUSED_RAYS; ++w) {
+      ds += part[w][0];
+      css += part[w][1];
+    }
+    *c.loss_out = col_term ? ds + (double)(c.w_color * (float)css) : ds;
   }
 }
+
+int64_t fused_loss_blocks(int64_t N) { return (N + FUSED_RAYS - 1) / FUSED_RAYS; }
 
 __device__ __forceinline__ void ray_grads_body(const RayCtx& c, int64_t block) {
   const int lane = threadIdx.x & 63;

@@ -372,7 +372,17 @@ class _GradBuffer:
     call takes the same buffer and views instead of building ~80 new views (the
     host cost of the drop-in path).  Entries are per (plan, stream, gradient set),
     so reuse is stream-ordered like the caching allocator's, and never used inside a
-    stream capture (memory captured into a graph stays in the graph's pool)."""
+    stream capture (memory captured into a graph stays in the graph's pool).
+
+    Stream contract: unlike the caching allocator the pool has no record_stream, so the
+    .grad tensors must be consumed on the render stream or on a stream that the render
+    stream waits on before the next forward (whose zero-fill rewrites a reused buffer).
+    The library's own consumers obey it: torch.optim and torch.distributed's collectives
+    (distributed.allreduce_grads / allreduce_rows_async: RCCL waits on the current stream
+    before it reads, and ``work.wait()`` makes the current stream wait on RCCL before the
+    caller goes on).  A caller that reads .grad on a user stream must make the render
+    stream wait on that stream (``torch.cuda.current_stream().wait_stream(s)``) before
+    the next render."""
 
     __slots__ = ("key", "buf", "gsize", "grid_grads", "flats", "pviews", "base")
 
@@ -466,8 +476,13 @@ def param_inputs(spec, plan, device, mode=None):
     leaf stands in for them, so ~80 AccumulateGrad nodes and Function inputs per call
     disappear from the host path; the reference's loops (loss.backward();
     optimizer.step(); optimizer.zero_grad(), Mapper.py:598-625, Tracker.py:113-135) see
-    the same .grad.  What it does not support: hooks on the decoder parameters,
-    torch.autograd.grad / backward(inputs=...) restricted to them.
+    the same .grad.  A backward that does not reach the parameters -- torch.autograd.grad
+    (loss, [camera]) as the Tracker's callers may write it, or backward(inputs=[...])
+    without them -- is detected (the engine will not execute the anchor's
+    AccumulateGrad node): the weight gradients are then neither computed (no k_mlp_dw)
+    nor written, as autograd would leave them.  What it does not support: hooks on the
+    decoder parameters, and torch.autograd.grad asked for the parameters themselves
+    (their gradient goes to .grad, not to the returned tuple: use "autograd" for that).
     ``"autograd"`` (``rendering: {param_grads: autograd}`` in the config, or
     ``NICECORE_PARAM_GRADS=autograd``): the parameters themselves, so their gradients
     reach ``.grad`` through AccumulateGrad like any autograd leaf (hooks,
@@ -486,6 +501,13 @@ def param_inputs(spec, plan, device, mode=None):
     if a is None:
         a = _ANCHORS[device] = torch.empty(0, device=device, requires_grad=True)
     return (a,)
+
+
+def _engine_reaches(anchor):
+    """Whether the running backward will execute the direct-mode anchor's AccumulateGrad
+    node, i.e. whether the decoder parameters are among the gradients it computes."""
+    node = torch.autograd.graph.get_gradient_edge(anchor).node
+    return bool(torch._C._will_engine_execute_node(node))
 
 
 def _attach(pairs):
@@ -522,6 +544,7 @@ class NiceRenderFn(torch.autograd.Function):
         pneeds = spec.get("param_needs")  # "direct" parameter gradients (param_inputs)
         ctx.direct = pneeds is not None
         ctx.n_param_inputs = len(params)
+        ctx.anchor = params[0] if (ctx.direct and params) else None
         if pneeds is None:
             pneeds = ctx.needs_input_grad[8:]
         else:
@@ -643,6 +666,9 @@ class NiceRenderFn(torch.autograd.Function):
             g_rd = g_rd if g_rd is not None else torch.empty_like(rays_o)
         a.g_rays_o, a.g_rays_d = _ptr(g_ro), _ptr(g_rd)
         needs_params = ctx.pneeds
+        skip_params = ctx.anchor is not None and not _engine_reaches(ctx.anchor)
+        if skip_params:  # autograd.grad / backward(inputs=) without the decoder parameters
+            needs_params = (False,) * len(needs_params)
         stream = _stream(device)
         e = ctx.grad_entry
         ctx.grad_entry = None  # a second backward (retain_graph) gets a fresh, zeroed buffer
@@ -652,6 +678,9 @@ class NiceRenderFn(torch.autograd.Function):
             if e.gsize:
                 e.buf[:e.gsize].zero_()
         e.bind(a, plan, ctx.sparse)
+        if skip_params:
+            for k in plan.decs:
+                a.dec[k].grad = None  # NULL decoder gradient: the library skips k_mlp_dw
         if rays_o.shape[0] == 0:  # empty batch: nothing is launched, every gradient is zero
             e.zero()
             grid_grads, pg = e.outputs(needs_params)

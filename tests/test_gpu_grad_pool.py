@@ -108,3 +108,29 @@ def test_direct_param_grads_graph_replay():
         step()
     torch.cuda.synchronize()
     _same(_grads(leaves), ref)
+
+
+@pytest.mark.gpu
+def test_direct_mode_autograd_grad_leaves_params_alone():
+    """param_grads="direct" under torch.autograd.grad(loss, [rays]) and backward(inputs=
+    [grid]): the decoder parameters are not among the requested gradients, so their .grad
+    stays None (k_mlp_dw is not launched), as autograd would leave it; the requested
+    gradients equal the full backward's."""
+    sc, g, model, ro, rd, gt, gtc, r = _setup()
+    leaves = _leaves(g, model, ro, rd)
+    _body_mode(r, g, model, ro, rd, gt, gtc, "direct")
+    full = _grads(leaves)
+    n0, n1 = len(g), len(g) + len(list(model.parameters()))
+    for t in leaves:
+        t.grad = None
+    d, u, c, L = r.render_batch_loss(g, model, rd, ro, "cuda", "color", gt, gtc, loss="mapper", color_term=True)
+    gro, grd = torch.autograd.grad(L, [ro, rd])
+    assert all(t.grad is None for t in leaves)
+    assert rel_err(gro.cpu(), full[-2].cpu()) <= 1e-6 and rel_err(grd.cpu(), full[-1].cpu()) <= 1e-6
+    d, u, c, L = r.render_batch_loss(g, model, rd, ro, "cuda", "color", gt, gtc, loss="mapper", color_term=True)
+    L.backward(inputs=[g["grid_fine"]])
+    got = _grads(leaves)
+    for i, t in enumerate(got):
+        if n0 <= i < n1:
+            assert t is None, i
+    assert rel_err(g["grid_fine"].grad.cpu(), full[list(g).index("grid_fine")].cpu()) <= 1e-6

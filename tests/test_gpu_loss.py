@@ -246,3 +246,32 @@ def test_no_weight_grad_flag_is_enforced(monkeypatch):
     L_ = r.render_batch_loss(g, model, rd, ro, "cuda", stage, gt, gtc, loss="mapper", color_term=True)[3]
     with pytest.raises(L.NiceCoreError, match="NC_NO_WEIGHT_GRAD"):
         L_.backward()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("color_term", [True, False])
+def test_fused_loss_value_fixed_order(color_term):
+    """k_composite_fwd_loss sums the loss in a fixed order (per-workgroup partials, the last
+    workgroup adds them in block order and applies w_color once to the float32 colour
+    total, as k_loss): the value is bit-identical from run to run and equals the
+    three-kernel path's (NC_DETERMINISTIC: k_loss) to float64 rounding for the depth term,
+    1e-6 relative with the float32 colour term."""
+    from nicecore import ops
+    from test_gpu_parity import _room0_case
+    n = 5000  # 313 workgroups of 16 rays
+    sc, grids, params, ro, rd, dep = _room0_case(n, "color", seed=12)
+    model = build_model(params, sc.bound, sc.bound * 2, "cuda")
+    g = {k: v.cuda().requires_grad_(True) for k, v in grids.items()}
+    c = dict(g)
+    ro, rd, gt = ro.cuda(), rd.cuda(), dep.cuda()
+    gtc = torch.rand(n, 3, generator=torch.Generator().manual_seed(4)).cuda()
+
+    def loss(det):
+        out = ops.render_rays_loss(model, c, ro, rd, sc.bound, "color", gt, loss="mapper", target_color=gtc,
+                                   w_color=0.2, color_term=color_term, deterministic=det)
+        return float(out[3].detach())
+    vals = [loss(None) for _ in range(4)]
+    assert len(set(vals)) == 1, vals
+    ref = loss(True)
+    tol = (1e-6 if color_term else 1e-13) * abs(ref)
+    assert abs(vals[0] - ref) <= tol, (vals[0], ref)

@@ -64,3 +64,30 @@ def test_renderer_reads_config_key():
     assert Renderer(cfg, None, slam).param_grads == "direct"
     del cfg["rendering"]["param_grads"]
     assert Renderer(cfg, None, slam).param_grads is None
+
+
+def test_engine_reach_of_the_anchor():
+    """render_fn._engine_reaches: True for loss.backward(), False for autograd.grad(loss,
+    [camera]) and backward(inputs=[...]) without the anchor -- the direct mode then
+    neither computes nor writes the decoder weight gradients."""
+    from nicecore.render_fn import _engine_reaches
+    anchor = torch.empty(0, requires_grad=True)
+    seen = []
+
+    class F(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, a):
+            return x * 2
+
+        @staticmethod
+        def backward(ctx, g):
+            seen.append(_engine_reaches(anchor))
+            return g * 2, None
+
+    cam = torch.ones(3, requires_grad=True)
+    x = torch.ones(3, requires_grad=True)
+    loss = F.apply(x * cam, anchor).sum()
+    torch.autograd.grad(loss, [cam], retain_graph=True)
+    loss.backward(inputs=[x], retain_graph=True)
+    loss.backward()
+    assert seen == [False, False, True]
