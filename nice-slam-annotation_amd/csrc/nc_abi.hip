@@ -513,6 +513,16 @@ int gather_and_claim(MlpCtx& m, const Ws& w, hipStream_t s) {
 // backward for d loss = 1 in one kernel (k_composite_fwd_loss; NICECORE_FUSED_LOSS=0 for
 // the three-kernel path).  Both sum the loss in a fixed order; NC_DETERMINISTIC keeps the
 // three-kernel path (k_loss's value, the reference's expression order).
+// NICECORE_FILL_IN_COMPOSITE=0: the fused forward's gradient zero fill stays in k_mlp_fwd (A/B)
+static bool fill_in_composite() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = std::getenv("NICECORE_FILL_IN_COMPOSITE");
+    on = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+  }
+  return on != 0;
+}
+
 bool fused_mapper_loss(const nc_render_args* a) {
   static int on = -1;
   if (on < 0) {
@@ -839,6 +849,15 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   }
   if (int e = gather_and_claim(m, w, s)) return e;
   if (!m.fuse_gather) {  // zeroed by k_grid_gather (else by k_mlp_fwd)
+    m.zero_fill = nullptr;
+    m.zero_n4 = 0;
+  } else if (rc.fuse_bwd && m.zero_fill && fill_in_composite()) {
+    // zeroed by k_composite_fwd_loss's extra workgroups instead: its rays occupy a quarter
+    // of the CUs, k_mlp_fwd's fill is a serial tail (every workgroup ends at once)
+    const int64_t nb = fused_loss_blocks(rc.N);
+    rc.zero_fill = m.zero_fill;
+    rc.zero_n4 = m.zero_n4;
+    rc.zero_wgs = (int32_t)std::max<int64_t>(64, cu_count() - nb);
     m.zero_fill = nullptr;
     m.zero_n4 = 0;
   }

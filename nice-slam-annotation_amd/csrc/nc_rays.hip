@@ -574,6 +574,13 @@ constexpr int FUSED_RAYS = NC_FUSED_RAYS;  // rays (waves) per workgroup: 63 ato
 
 __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const RayCtx c) {
   __shared__ double part[FUSED_RAYS][2];
+  const unsigned nb = (unsigned)((c.N + FUSED_RAYS - 1) / FUSED_RAYS);  // ray workgroups
+  if (blockIdx.x >= nb) {  // the gradient buffer's zero fill on the CUs the rays leave idle
+    const int64_t nthr = (int64_t)c.zero_wgs * blockDim.x;
+    for (int64_t z = (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x; z < c.zero_n4; z += nthr)
+      c.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t r = (int64_t)blockIdx.x * FUSED_RAYS + wv;
   const bool col_term = (c.loss_flags & NC_LOSS_COLOR) != 0;
@@ -623,7 +630,7 @@ __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const Ra
     c.loss_part[2 * blockIdx.x] = d;
     c.loss_part[2 * blockIdx.x + 1] = cs;
     __threadfence();  // the partials are visible device-wide before the count says so
-    last = atomicAdd(c.loss_count, 1u) == gridDim.x - 1;
+    last = atomicAdd(c.loss_count, 1u) == nb - 1;
   }
   __syncthreads();
   if (!last) return;
@@ -631,7 +638,7 @@ __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const Ra
   // the last workgroup: every partial in block order (thread t: blocks t, t + 64 * FUSED_RAYS,
   // ...), then the wave butterfly and the waves in order -- one association for any timing
   double d = 0.0, cs = 0.0;
-  for (unsigned b = threadIdx.x; b < gridDim.x; b += 64 * FUSED_RAYS) {
+  for (unsigned b = threadIdx.x; b < nb; b += 64 * FUSED_RAYS) {
     d += c.loss_part[2 * b];
     cs += c.loss_part[2 * b + 1];
   }
@@ -807,7 +814,8 @@ int launch_composite_fwd(const RayCtx& c, hipStream_t s) {
   return (int)hipGetLastError();
 }
 int launch_composite_fwd_loss(const RayCtx& c, hipStream_t s) {
-  hipLaunchKernelGGL(k_composite_fwd_loss, dim3((unsigned)((c.N + FUSED_RAYS - 1) / FUSED_RAYS)), dim3(64 * FUSED_RAYS), 0,
+  const unsigned nb = (unsigned)((c.N + FUSED_RAYS - 1) / FUSED_RAYS);
+  hipLaunchKernelGGL(k_composite_fwd_loss, dim3(nb + (c.zero_fill ? (unsigned)c.zero_wgs : 0u)), dim3(64 * FUSED_RAYS), 0,
                      s, c);
   return (int)hipGetLastError();
 }
