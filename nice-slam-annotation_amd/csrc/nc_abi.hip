@@ -513,14 +513,18 @@ int gather_and_claim(MlpCtx& m, const Ws& w, hipStream_t s) {
 // backward for d loss = 1 in one kernel (k_composite_fwd_loss; NICECORE_FUSED_LOSS=0 for
 // the three-kernel path).  Both sum the loss in a fixed order; NC_DETERMINISTIC keeps the
 // three-kernel path (k_loss's value, the reference's expression order).
-// NICECORE_FILL_IN_COMPOSITE=0: the fused forward's gradient zero fill stays in k_mlp_fwd (A/B)
-static bool fill_in_composite() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = std::getenv("NICECORE_FILL_IN_COMPOSITE");
-    on = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+// The fused mapper forward's gradient zero fill: -1 = at k_mlp_fwd's tail, else the
+// percentage filled by k_ray_setup's extra workgroups (the rest by k_composite_fwd_loss's).
+// NICECORE_FILL_SETUP_PCT=<0..100> or "fwd" (A/B).
+static int fill_in_composite() {
+  static int pct = -2;
+  if (pct == -2) {
+    const char* e = std::getenv("NICECORE_FILL_SETUP_PCT");
+    pct = 0;
+    if (e && std::strcmp(e, "fwd") == 0) pct = -1;
+    else if (e && *e) pct = std::max(0, std::min(100, std::atoi(e)));
   }
-  return on != 0;
+  return pct;
 }
 
 bool fused_mapper_loss(const nc_render_args* a) {
@@ -832,7 +836,6 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
       return e;
     }
   }
-  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
   MlpCtx m;
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
   for (int j = 0; j < m.n_jobs; ++j)  // NC_NO_WEIGHT_GRAD: no activation records for k_mlp_dw
@@ -847,17 +850,24 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     m.zero_fill = reinterpret_cast<float4*>(a->grad_zero);
     m.zero_n4 = a->grad_zero_floats / 4;
   }
-  if (int e = gather_and_claim(m, w, s)) return e;
-  if (!m.fuse_gather) {  // zeroed by k_grid_gather (else by k_mlp_fwd)
-    m.zero_fill = nullptr;
-    m.zero_n4 = 0;
-  } else if (rc.fuse_bwd && m.zero_fill && fill_in_composite()) {
-    // zeroed by k_composite_fwd_loss's extra workgroups instead: its rays occupy a quarter
-    // of the CUs, k_mlp_fwd's fill is a serial tail (every workgroup ends at once)
+  if (w.fuse && rc.fuse_bwd && m.zero_fill && fill_in_composite() >= 0) {
+    // zeroed on the CUs the per-ray kernels leave idle instead of at k_mlp_fwd's tail (a
+    // serial tail: every workgroup of its one resident wave ends at once): the first
+    // fill_in_composite() percent by extra workgroups of k_ray_setup, the rest by extra
+    // workgroups of k_composite_fwd_loss
     const int64_t nb = fused_loss_blocks(rc.N);
     rc.zero_fill = m.zero_fill;
     rc.zero_n4 = m.zero_n4;
+    rc.zero_lo4 = (m.zero_n4 * fill_in_composite() / 100 + 63) & ~int64_t(63);
+    if (rc.zero_lo4 > rc.zero_n4) rc.zero_lo4 = rc.zero_n4;
     rc.zero_wgs = (int32_t)std::max<int64_t>(64, cu_count() - nb);
+    rc.zero_wgs_setup = cu_count();
+    m.zero_fill = nullptr;
+    m.zero_n4 = 0;
+  }
+  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
+  if (int e = gather_and_claim(m, w, s)) return e;
+  if (!m.fuse_gather) {  // zeroed by k_grid_gather (else by k_mlp_fwd)
     m.zero_fill = nullptr;
     m.zero_n4 = 0;
   }

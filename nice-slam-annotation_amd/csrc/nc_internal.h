@@ -179,9 +179,12 @@ struct RayCtx {
   const uint8_t* valid;      // [N] nc_render_args.ray_valid (0 = ray dropped), or NULL
   double* loss_part;         // fused loss: [fused_loss_blocks(N)][2] per-workgroup (depth, colour) sums
   unsigned* loss_count;      // fused loss: workgroups done (zeroed by k_ray_setup; the last one sums)
-  float4* zero_fill;         // fused loss: the backward's gradient buffer, zero-filled by zero_wgs extra
-  int64_t zero_n4;           // workgroups of k_composite_fwd_loss (the CUs its rays leave idle)
-  int32_t zero_wgs;
+  // fused loss: the backward's gradient buffer, zero-filled on the CUs the per-ray kernels
+  // leave idle: float4s [0, zero_lo4) by zero_wgs_setup extra workgroups of k_ray_setup,
+  // [zero_lo4, zero_n4) by zero_wgs extra workgroups of k_composite_fwd_loss
+  float4* zero_fill;
+  int64_t zero_n4, zero_lo4;
+  int32_t zero_wgs, zero_wgs_setup;
 };
 
 // k_composite_fwd_loss workgroups for N rays (the length of RayCtx::loss_part)

@@ -52,6 +52,13 @@ __device__ __forceinline__ double max_nan(double a, double b) { return (a > b ||
 __device__ __forceinline__ double min_nan(double a, double b) { return (a < b || isnan(a)) ? a : b; }
 
 __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
+  const unsigned nb = (unsigned)((c.N + RAY_WAVES - 1) / RAY_WAVES);  // ray workgroups
+  if (blockIdx.x >= nb) {  // the first part of the gradient buffer's zero fill (RayCtx::zero_lo4)
+    const int64_t nthr = (int64_t)c.zero_wgs_setup * blockDim.x;
+    for (int64_t z = (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x; z < c.zero_lo4; z += nthr)
+      c.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x < MAX_JOBS && c.range_flag) c.range_flag[threadIdx.x] = 0u;  // for k_mlp_fwd
@@ -577,7 +584,7 @@ __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const Ra
   const unsigned nb = (unsigned)((c.N + FUSED_RAYS - 1) / FUSED_RAYS);  // ray workgroups
   if (blockIdx.x >= nb) {  // the gradient buffer's zero fill on the CUs the rays leave idle
     const int64_t nthr = (int64_t)c.zero_wgs * blockDim.x;
-    for (int64_t z = (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x; z < c.zero_n4; z += nthr)
+    for (int64_t z = c.zero_lo4 + (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x; z < c.zero_n4; z += nthr)
       c.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
     return;
   }
@@ -806,7 +813,8 @@ int launch_depth_max(const float* gt, const uint8_t* valid, int64_t n, float* ou
   return (int)hipGetLastError();
 }
 int launch_ray_setup(const RayCtx& c, hipStream_t s) {
-  hipLaunchKernelGGL(k_ray_setup, dim3(ray_blocks(c.N)), dim3(256), 0, s, c);
+  hipLaunchKernelGGL(k_ray_setup, dim3(ray_blocks(c.N) + (c.zero_fill && c.zero_lo4 > 0 ? (unsigned)c.zero_wgs_setup : 0u)),
+                     dim3(256), 0, s, c);
   return (int)hipGetLastError();
 }
 int launch_composite_fwd(const RayCtx& c, hipStream_t s) {
@@ -815,7 +823,8 @@ int launch_composite_fwd(const RayCtx& c, hipStream_t s) {
 }
 int launch_composite_fwd_loss(const RayCtx& c, hipStream_t s) {
   const unsigned nb = (unsigned)((c.N + FUSED_RAYS - 1) / FUSED_RAYS);
-  hipLaunchKernelGGL(k_composite_fwd_loss, dim3(nb + (c.zero_fill ? (unsigned)c.zero_wgs : 0u)), dim3(64 * FUSED_RAYS), 0,
+  hipLaunchKernelGGL(k_composite_fwd_loss, dim3(nb + (c.zero_fill && c.zero_n4 > c.zero_lo4 ? (unsigned)c.zero_wgs : 0u)),
+                     dim3(64 * FUSED_RAYS), 0,
                      s, c);
   return (int)hipGetLastError();
 }

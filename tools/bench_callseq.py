@@ -2,10 +2,12 @@
 fused and the graph-replayed steps (what a caller that keeps the
 reference's Python loss gets).
 
-    ref     Renderer.render_batch_ray + the reference's loss expression with its boolean
-            masks (Mapper.py:598-612) + loss.backward()
-    fused   Renderer.render_batch_loss + backward (bench.py's eager step)
-    graph   the fused step replayed from a hipGraph (bench.py's value)
+    ref        Renderer.render_batch_ray + the reference's loss expression with its boolean
+               masks (Mapper.py:598-612) + loss.backward()
+    loss_only  ref's loss statement + backward over precomputed render outputs: the
+               caller's own share of ref (a render that cost nothing)
+    fused      Renderer.render_batch_loss + backward (bench.py's eager step)
+    graph      the fused step replayed from a hipGraph (bench.py's value)
 
 Run on a GPU box:  python tools/bench_callseq.py [--steps 200] [--profile]"""
 import cProfile
@@ -65,9 +67,23 @@ def main():
               for a, b in zip(ga, gb) if a is not None)
     print(f"ref loss {la:.9e} fused loss {lb:.9e} rel {abs(la - lb) / abs(lb):.2e}; max grad rel err {err:.2e}")
 
+    # the caller's own part of ref(): the same loss statement and backward over
+    # precomputed render outputs (leaves), i.e. ref() with a render that costs nothing
+    d0, u0, c0 = (t.detach() for t in r.render_batch_ray(grids, model, rd, ro, device, stage, gt))
+    dl, cl = d0.clone().requires_grad_(True), c0.clone().requires_grad_(True)
+
+    def loss_only():
+        dl.grad = cl.grad = None
+        depth_mask = gt > 0
+        loss = torch.abs(gt[depth_mask] - dl[depth_mask]).sum()
+        if stage == "color":
+            loss += w_color * torch.abs(gtc - cl).sum()
+        loss.backward()
+        return loss
+
     graph = GraphedStep(fused)
     res = {}
-    for name, fn in (("ref", ref), ("fused", fused), ("graph", graph), ("ref", ref)):
+    for name, fn in (("ref", ref), ("fused", fused), ("graph", graph), ("ref", ref), ("loss_only", loss_only)):
         for _ in range(args.warmup + 5):
             fn()
         torch.cuda.synchronize()
@@ -78,7 +94,7 @@ def main():
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         res[name] = (1e3 * (t2 - t0) / args.steps, 1e3 * (t1 - t0) / args.steps)
-        print(f"{name:6s} wall {res[name][0]:.4f} ms/step  host enqueue {res[name][1]:.4f} ms/step", flush=True)
+        print(f"{name:9s} wall {res[name][0]:.4f} ms/step  host enqueue {res[name][1]:.4f} ms/step", flush=True)
     if prof:
         pr = cProfile.Profile()
         pr.enable()
