@@ -66,6 +66,7 @@ VARIANTS = {
     "dw_none": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_STAGE", "-DNC_ABL_DW_NO_EMB", "-DNC_ABL_DW_NO_MASKPASS",
                 "-DNC_ABL_DW_NO_LOAD", "-DNC_ABL_DW_NO_MFMA"],
     "dw_serial_nomfma": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_MFMA"],
+    "dw_split16": ["-DNC_DW_SPLIT16"],
 }
 # variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
 
