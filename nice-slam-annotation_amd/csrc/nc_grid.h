@@ -65,7 +65,8 @@ __device__ __forceinline__ void grid_coord_grad(const nc_grid& G, const Corners&
 // face-adjacent cell carries the shared face over.  Sparse gradient rows
 // (G.grad_rows): a corner's destination is its voxel's row instead of its voxel.
 // Slice layout (floats), padded so the per-lane writes of the 16 points spread over
-// the LDS banks: D [16][36] (row pad 4), Wt / OFF transposed [corner][17].
+// the LDS banks: D [16][36] (row pad 4), Wt [x side][point][(y, z)] (one float4 per
+// point and side in the walk), OFF transposed [corner][17].
 constexpr int SCAT_DLD = 36, SCAT_KLD = 17;
 constexpr int SCAT_WT = 16 * SCAT_DLD;             // 576
 constexpr int SCAT_OFF = SCAT_WT + 8 * SCAT_KLD;   // 712 (8-B aligned)
@@ -78,7 +79,7 @@ static_assert(SCAT_FLOATS % 4 == 0 && SCAT_OFF % 2 == 0 && SCAT_KEY % 2 == 0, "s
 __device__ __forceinline__ void grid_scatter_stage(const nc_grid& G, const Corners& c, const float dc[8], bool valid,
                                                    float* reg, int i, int g) {
   float* D = reg;                                              // [16][36] d features
-  float* Wt = reg + SCAT_WT;                                   // [8][17] corner weights
+  float* Wt = reg + SCAT_WT;                                   // [2 x side][16][4 (y, z)] corner weights
   int64_t* OFF = reinterpret_cast<int64_t*>(reg + SCAT_OFF);   // [8][17] grad-corner offsets
   int64_t* KEY = reinterpret_cast<int64_t*>(reg + SCAT_KEY);   // [16] voxel-cell key (-1: none)
   int* INB = reinterpret_cast<int*>(reg + SCAT_INB);           // [16] in-bounds corner mask
@@ -88,8 +89,8 @@ __device__ __forceinline__ void grid_scatter_stage(const nc_grid& G, const Corne
     const int yb = g & 1, zb = g >> 1;
     const float wy = yb ? c.wy[1] : c.wy[0];
     const float wz = zb ? c.wz[1] : c.wz[0];
-    Wt[(2 * g) * SCAT_KLD + i] = (c.wx[0] * wy) * wz;
-    Wt[(2 * g + 1) * SCAT_KLD + i] = (c.wx[1] * wy) * wz;
+    Wt[4 * i + g] = (c.wx[0] * wy) * wz;  // corner k = 2 g: x side 0, (y, z) = g
+    Wt[64 + 4 * i + g] = (c.wx[1] * wy) * wz;
     if (G.grad_rows) {  // sparse gradient rows: the rows the forward claimed (-1: none, skipped)
       const int64_t v = ((int64_t)(c.z0 + zb) * G.dims[1] + (c.y0 + yb)) * G.dims[2] + c.x0;
       const int k0 = 2 * g, k1 = 2 * g + 1;
@@ -123,10 +124,17 @@ __device__ __forceinline__ void grid_scatter_flush(const nc_grid& G, const float
   auto flush = [&](int pt, int xb, int q, float v) {
     const int k = xb | (q << 1);
     const int64_t o = OFF[k * SCAT_KLD + pt];
+#ifdef NC_ABL_DX_NO_ATOMIC  // timing-only ablation: the walk without its atomics (o is never -7)
+    if (((INB[pt] >> k) & 1) && o == -7) atomicAdd(G.grad + o + chs, v);
+#else
     if (((INB[pt] >> k) & 1) && o >= 0) atomicAdd(G.grad + o + chs, v);
+#endif
   };
   int run = 0;
   int64_t cur = KEY[0];
+#ifdef NC_SCAT_UNROLL
+#pragma unroll NC_SCAT_UNROLL
+#endif
   for (int pt = 0; pt < 16; ++pt) {
     const int64_t kk = KEY[pt];  // wave-uniform
     if (kk != cur) {
@@ -171,8 +179,11 @@ __device__ __forceinline__ void grid_scatter_flush(const nc_grid& G, const float
       cur = kk;
     }
     const float dv = D[pt * SCAT_DLD + ch];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = acc[q] + Wt[(half + 2 * q) * SCAT_KLD + pt] * dv;
+    const float4 w = *reinterpret_cast<const float4*>(Wt + 64 * half + 4 * pt);  // one read: this side's 4 corners
+    acc[0] = acc[0] + w.x * dv;
+    acc[1] = acc[1] + w.y * dv;
+    acc[2] = acc[2] + w.z * dv;
+    acc[3] = acc[3] + w.w * dv;
     run = pt;
   }
 #pragma unroll

@@ -67,6 +67,9 @@ VARIANTS = {
                 "-DNC_ABL_DW_NO_LOAD", "-DNC_ABL_DW_NO_MFMA"],
     "dw_serial_nomfma": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_MFMA"],
     "dw_split16": ["-DNC_DW_SPLIT16"],
+    "scat_u2": ["-DNC_SCAT_UNROLL=2"],
+    "scat_u4": ["-DNC_SCAT_UNROLL=4"],
+    "scat_u16": ["-DNC_SCAT_UNROLL=16"],
 }
 # variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
 
