@@ -516,7 +516,7 @@ int gather_and_claim(MlpCtx& m, const Ws& w, hipStream_t s) {
 // The fused mapper forward's gradient zero fill: -1 = at k_mlp_fwd's tail, else the
 // percentage filled by k_ray_setup's extra workgroups (the rest by k_composite_fwd_loss's).
 // NICECORE_FILL_SETUP_PCT=<0..100> or "fwd" (A/B).
-static int fill_in_composite() {
+static int fill_setup_pct() {
   static int pct = -2;
   if (pct == -2) {
     const char* e = std::getenv("NICECORE_FILL_SETUP_PCT");
@@ -850,15 +850,15 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     m.zero_fill = reinterpret_cast<float4*>(a->grad_zero);
     m.zero_n4 = a->grad_zero_floats / 4;
   }
-  if (w.fuse && rc.fuse_bwd && m.zero_fill && fill_in_composite() >= 0) {
+  if (w.fuse && rc.fuse_bwd && m.zero_fill && fill_setup_pct() >= 0) {
     // zeroed on the CUs the per-ray kernels leave idle instead of at k_mlp_fwd's tail (a
     // serial tail: every workgroup of its one resident wave ends at once): the first
-    // fill_in_composite() percent by extra workgroups of k_ray_setup, the rest by extra
+    // fill_setup_pct() percent by extra workgroups of k_ray_setup, the rest by extra
     // workgroups of k_composite_fwd_loss
     const int64_t nb = fused_loss_blocks(rc.N);
     rc.zero_fill = m.zero_fill;
     rc.zero_n4 = m.zero_n4;
-    rc.zero_lo4 = (m.zero_n4 * fill_in_composite() / 100 + 63) & ~int64_t(63);
+    rc.zero_lo4 = (m.zero_n4 * fill_setup_pct() / 100 + 63) & ~int64_t(63);
     if (rc.zero_lo4 > rc.zero_n4) rc.zero_lo4 = rc.zero_n4;
     rc.zero_wgs = (int32_t)std::max<int64_t>(64, cu_count() - nb);
     rc.zero_wgs_setup = cu_count();

@@ -120,23 +120,43 @@ __device__ __forceinline__ void grid_scatter_flush(const nc_grid& G, const float
   const int* INB = reinterpret_cast<const int*>(reg + SCAT_INB);
   const int half = lane >> 5, ch = lane & 31;
   const int64_t chs = G.grad_rows ? (int64_t)ch : (int64_t)ch * stride32(G.grad_stride[0]);
+  // the cell keys and in-bounds masks are per point, the same in every lane: read them
+  // into scalar registers, so the walk's run / face-shift decisions are scalar branches
+  auto key_at = [&](int pt) -> int64_t {
+    const uint64_t v = (uint64_t)KEY[pt];
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  };
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  auto flush = [&](int pt, int xb, int q, float v) {
-    const int k = xb | (q << 1);
-    const int64_t o = OFF[k * SCAT_KLD + pt];
+  // up to four corner rows of point pt: every destination offset is read before the first
+  // atomic is issued (one LDS wait per group, not one per atomic)
+  auto flush_n = [&](int pt, int n, const int* k, const float* v) {
+    int64_t o[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      if (a < n) o[a] = OFF[k[a] * SCAT_KLD + pt];
+    const unsigned inb = __builtin_amdgcn_readfirstlane(INB[pt]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      if (a >= n) break;
 #ifdef NC_ABL_DX_NO_ATOMIC  // timing-only ablation: the walk without its atomics (o is never -7)
-    if (((INB[pt] >> k) & 1) && o == -7) atomicAdd(G.grad + o + chs, v);
+      if (((inb >> k[a]) & 1u) && o[a] == -7) atomicAdd(G.grad + o[a] + chs, v[a]);
 #else
-    if (((INB[pt] >> k) & 1) && o >= 0) atomicAdd(G.grad + o + chs, v);
+      if (((inb >> k[a]) & 1u) && o[a] >= 0) atomicAdd(G.grad + o[a] + chs, v[a]);
 #endif
+    }
   };
   int run = 0;
-  int64_t cur = KEY[0];
+  int64_t cur = key_at(0);
 #ifdef NC_SCAT_UNROLL
 #pragma unroll NC_SCAT_UNROLL
 #endif
   for (int pt = 0; pt < 16; ++pt) {
-    const int64_t kk = KEY[pt];  // wave-uniform
+    const int64_t kk = key_at(pt);  // wave-uniform
+    // this point's d feature and corner weights, read before a run flush can wait on LDS
+    const float dv = D[pt * SCAT_DLD + ch];
+    const float4 w = *reinterpret_cast<const float4*>(Wt + 64 * half + 4 * pt);  // one read: this side's 4 corners
     if (kk != cur) {
       const int64_t d = kk - cur;
       int axis = -1, dir = 0;
@@ -149,49 +169,68 @@ __device__ __forceinline__ void grid_scatter_flush(const nc_grid& G, const float
         else if (d == -(int64_t(1) << 42)) { axis = 2; dir = -1; }
       }
       if (axis < 0) {
+        const int k[4] = {half, half | 2, half | 4, half | 6};
+        flush_n(run, 4, k, acc);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          flush(run, half, q, acc[q]);
-          acc[q] = 0.f;
-        }
+        for (int q = 0; q < 4; ++q) acc[q] = 0.f;
       } else if (axis == 0) {
         const int L = dir > 0 ? 0 : 1;
         float mv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) mv[q] = __shfl_xor(acc[q], 32);
         const bool onL = half == L;
-        flush(run, L, onL ? 0 : 2, onL ? acc[0] : mv[2]);
-        flush(run, L, onL ? 1 : 3, onL ? acc[1] : mv[3]);
+        const int k[2] = {L | ((onL ? 0 : 2) << 1), L | ((onL ? 1 : 3) << 1)};
+        const float v[2] = {onL ? acc[0] : mv[2], onL ? acc[1] : mv[3]};
+        flush_n(run, 2, k, v);
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = onL ? mv[q] : 0.f;
       } else {
+        // the two (y, z) corners on the far side of the shared face leave (the axis and
+        // direction are scalar: which two q is the same in every lane)
         const int qb = axis;
-        float nacc[4];
+        int k[2], n = 0;
+        float v[2], nacc[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const bool other = ((q & qb) != 0) == (dir < 0);
-          if (other) flush(run, half, q, acc[q]);
+          if (other) {
+            k[n & 1] = half | (q << 1);
+            v[n & 1] = acc[q];
+            ++n;
+          }
           nacc[q] = other ? acc[q ^ qb] : 0.f;
         }
+        flush_n(run, 2, k, v);
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = nacc[q];
       }
       cur = kk;
     }
-    const float dv = D[pt * SCAT_DLD + ch];
-    const float4 w = *reinterpret_cast<const float4*>(Wt + 64 * half + 4 * pt);  // one read: this side's 4 corners
     acc[0] = acc[0] + w.x * dv;
     acc[1] = acc[1] + w.y * dv;
     acc[2] = acc[2] + w.z * dv;
     acc[3] = acc[3] + w.w * dv;
     run = pt;
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) flush(run, half, q, acc[q]);
+  {
+    const int k[4] = {half, half | 2, half | 4, half | 6};
+    flush_n(run, 4, k, acc);
+  }
+}
+
+// the lane id computed where it is used (volatile: not hoisted out of the tile loop).
+// k_mlp_dx runs at its register cap: the staging's per-lane LDS addresses, kept live
+// across the tile loop, were spilled and each reload waited vmcnt(0) -- behind the
+// tile's record / point-gradient stores and corner loads
+__device__ __forceinline__ int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
 }
 
 __device__ __forceinline__ void grid_scatter(const nc_grid& G, const Corners& c, const float dc[8], bool valid,
-                                             float* reg, int i, int g, int lane) {
+                                             float* reg, int, int, int) {
+  const int lane = lane_here(), i = lane & 15, g = lane >> 4;
   grid_scatter_stage(G, c, dc, valid, reg, i, g);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -879,7 +879,8 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
   float* bacc = lds + DX_BACC + wave * DX_BSLAB;  // this wave's d fourier_B (xyz decoders, weight gradients)
   for (int e = threadIdx.x; e < waves * DX_BSLAB; e += blockDim.x) lds[DX_BACC + e] = 0.f;  // ordered by load_weights' barrier
   load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
-  float* slice = lds + DX_SLICE_BASE + wave * SCAT_FLOATS;  // this wave's scatter staging
+  // this wave's scatter staging (a scalar base: nothing per lane to keep live across tiles)
+  float* slice = lds + DX_SLICE_BASE + __builtin_amdgcn_readfirstlane(wave) * SCAT_FLOATS;
   const int64_t ntiles = (ctx.P + 15) / 16;
   const float dscale = ctx.dout_scale ? (float)*ctx.dout_scale : 1.f;  // fused mapper loss: d loss
   for (int64_t t = (int64_t)blockIdx.x * waves + wave; t < ntiles; t += (int64_t)gridDim.x * waves) {
