@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 session n: k_mlp_dx scatter walk: float4 weights (w4), + scalar cell keys (skey), + destination offsets read before the atomics of a group (batch), + the point's d feature and weights read before the flush (hoist), + lane ids recomputed in the scatter, scalar slice base: no spill reloads (lane)
+# round 4 session n: k_mlp_dx with the tile's p.float() and coordinate loads issued before its record stores (early) against the committed build (lane)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r4n
@@ -10,4 +10,4 @@ step() { # name seconds cmd...
   echo "[$n] rc=$rc"; tail -12 $O/$n.log | cut -c1-400
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step ab 600 python3 -u tools/ablate.py run w4 hoist lane w4 hoist lane
+step ab 600 python3 -u tools/ablate.py run lane early lane early lane early
