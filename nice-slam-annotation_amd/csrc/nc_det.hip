@@ -116,12 +116,12 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   const int64_t s = (int64_t)blockIdx.x * 8 + hw;
   const int64_t e0 = s * DSUB;
   const int cnt = e0 >= n ? 0 : (int)(n - e0 < DSUB ? n - e0 : DSUB);
-  const K* key = reinterpret_cast<const K*>(d.key[d.sorted]);
+  const K* key = reinterpret_cast<const K*>(d.sorted ? d.key[1] : d.key[0]);  // select: a runtime index into the argument copies it to scratch
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   // the sub-chunk's entries, one per lane (coalesced), then every entry's weighted
   // feature-gradient row in flight at once
   const K myk = ch < cnt ? key[e0 + ch] : invalid;
-  const uint32_t ent = ch < cnt ? d.val[d.sorted][e0 + ch] : 0u;
+  const uint32_t ent = ch < cnt ? (d.sorted ? d.val[1] : d.val[0])[e0 + ch] : 0u;
   const float myw = ch < cnt ? d.w[ent] : 0.f;
   float v[DSUB];
 #pragma unroll
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
   const int64_t e0 = s * DSUB;
   if (e0 >= n) return;
   const int64_t e1 = e0 + DSUB < n ? e0 + DSUB : n;
-  const K* key = reinterpret_cast<const K*>(d.key[d.sorted]);
+  const K* key = reinterpret_cast<const K*>(d.sorted ? d.key[1] : d.key[0]);  // select: a runtime index into the argument copies it to scratch
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   const K last = key[e1 - 1];
   if (last == invalid || e1 >= n || key[e1] != last) return;  // no run continues past s
