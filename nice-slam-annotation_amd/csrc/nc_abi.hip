@@ -860,7 +860,10 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     rc.zero_n4 = m.zero_n4;
     rc.zero_lo4 = (m.zero_n4 * fill_setup_pct() / 100 + 63) & ~int64_t(63);
     if (rc.zero_lo4 > rc.zero_n4) rc.zero_lo4 = rc.zero_n4;
-    rc.zero_wgs = (int32_t)std::max<int64_t>(64, cu_count() - nb);
+#ifndef NC_FILL_WGS_PER_CU
+#define NC_FILL_WGS_PER_CU 1
+#endif
+    rc.zero_wgs = (int32_t)std::max<int64_t>(64, NC_FILL_WGS_PER_CU * cu_count() - nb);
     rc.zero_wgs_setup = cu_count();
     m.zero_fill = nullptr;
     m.zero_n4 = 0;

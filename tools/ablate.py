@@ -67,6 +67,8 @@ VARIANTS = {
                 "-DNC_ABL_DW_NO_LOAD", "-DNC_ABL_DW_NO_MFMA"],
     "dw_serial_nomfma": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_MFMA"],
     "dw_split16": ["-DNC_DW_SPLIT16"],
+    "fill2": ["-DNC_FILL_WGS_PER_CU=2"],
+    "fill3": ["-DNC_FILL_WGS_PER_CU=3"],
     "scat_u2": ["-DNC_SCAT_UNROLL=2"],
     "scat_u4": ["-DNC_SCAT_UNROLL=4"],
     "scat_u16": ["-DNC_SCAT_UNROLL=16"],

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 session n: k_mlp_dx with the tile's p.float() and coordinate loads issued before its record stores (early) against the committed build (lane)
+# round 4 session n: zero-fill workgroups per CU in k_composite_fwd_loss (1, 2, 3)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r4n
@@ -10,4 +10,4 @@ step() { # name seconds cmd...
   echo "[$n] rc=$rc"; tail -12 $O/$n.log | cut -c1-400
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step ab 600 python3 -u tools/ablate.py run lane early lane early lane early
+step ab 600 python3 -u tools/ablate.py run cur fill2 fill3 cur fill2 fill3
