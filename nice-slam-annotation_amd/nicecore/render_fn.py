@@ -505,9 +505,14 @@ def param_inputs(spec, plan, device, mode=None):
 
 def _engine_reaches(anchor):
     """Whether the running backward will execute the direct-mode anchor's AccumulateGrad
-    node, i.e. whether the decoder parameters are among the gradients it computes."""
-    node = torch.autograd.graph.get_gradient_edge(anchor).node
-    return bool(torch._C._will_engine_execute_node(node))
+    node, i.e. whether the decoder parameters are among the gradients it computes.  A
+    torch without the query (a private engine API) is answered "yes": the parameters'
+    .grad is written, the behaviour before the check existed."""
+    try:
+        node = torch.autograd.graph.get_gradient_edge(anchor).node
+        return bool(torch._C._will_engine_execute_node(node))
+    except (AttributeError, RuntimeError):
+        return True
 
 
 def _attach(pairs):
