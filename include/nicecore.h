@@ -176,9 +176,9 @@ typedef struct nc_render_args {
    * tracker loss detached, as in the reference).  NC_LOSS_MAPPER with
    * NC_SAVE_FOR_BACKWARD (and not NC_DETERMINISTIC): the forward also forms the loss's
    * d raw for d loss = 1 and the backward scales it by *g_loss when that is the only
-   * upstream gradient (no k_loss / k_composite_bwd); *loss_out is then a sum of float64
-   * per-workgroup partials whose last bits depend on their order (NC_DETERMINISTIC: fixed
-   * order). */
+   * upstream gradient (no k_loss / k_composite_bwd); *loss_out is then the float64
+   * per-workgroup partials added in block order by the last workgroup (fixed order,
+   * identical run to run; w_color applied once to the float32 colour total). */
   int32_t loss;             /* NC_LOSS_* */
   int32_t loss_flags;       /* NC_LOSS_COLOR | NC_LOSS_DYNAMIC */
   double w_color;           /* w_color_loss (applied in float32, as the reference) */
