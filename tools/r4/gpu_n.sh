@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 session n: k_mlp_dw with two wave groups alternating staging and k-steps (1024 and 768 threads)
+# round 4 session n: k_mlp_dx with the tile's p.float() and coordinates parked in LDS at the tile start (park) against the committed build (lane)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r4n
@@ -10,4 +10,4 @@ step() { # name seconds cmd...
   echo "[$n] rc=$rc"; tail -12 $O/$n.log | cut -c1-400
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step ab 600 python3 -u tools/ablate.py run cur dw_g2 dw_g2_768 cur dw_g2 dw_g2_768
+step ab 600 python3 -u tools/ablate.py run lane park lane park lane park
