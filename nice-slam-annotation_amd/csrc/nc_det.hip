@@ -106,8 +106,36 @@ __device__ __forceinline__ void det_add(const MlpCtx& m, const DetBufs& d, uint6
   if (dst) *dst = *dst + acc;
 }
 
+// The gradient row of voxel key k0 resolved through per-job descriptors read once per
+// launch (job and grid are uniform there, so they sit in scalar registers): the run loop
+// then selects among them per run instead of indexing the kernel argument with a
+// per-lane job, which the compiler turns into dependent vector loads of the argument.
+struct DetRows {
+  float* grad[3];
+  const int32_t* rows[3];  // sparse gradient rows, or nullptr: dense channels-last rows
+  bool fast;               // every job with a grid gradient has sparse or packed dense rows
+};
+__device__ __forceinline__ DetRows det_rows(const MlpCtx& m) {
+  DetRows r;
+  r.fast = true;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const Job job = job_of(m, j);
+    const nc_grid G = grid_of(m, job.kind);
+    const int64_t H = G.dims[1], W = G.dims[2];
+    r.grad[j] = G.grad;
+    r.rows[j] = G.grad_rows;
+    const bool packed = G.grad_stride[0] == 1 && G.grad_stride[3] == 32 && G.grad_stride[2] == 32 * W &&
+                        G.grad_stride[1] == 32 * W * H;
+    r.fast = r.fast && (!job.need_grid || G.grad_rows || packed);
+  }
+  return r;
+}
+
 // half-wave = sub-chunk s (entries [32 s, 32 s + 32)), lane = channel.  The run sums are
-// formed in registers, parked in LDS, then written by one loop over the runs.
+// formed in registers, parked in LDS, then written by one loop over the runs.  Every load
+// is unconditional (clamped index, result selected afterwards): a load under a branch is
+// issued alone and waited for, which made each of the 32 row gathers a serial latency.
 template <typename K>
 __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int64_t n) {
   __shared__ float racc[8][DSUB][32];
@@ -117,18 +145,25 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   const int64_t e0 = s * DSUB;
   const int cnt = e0 >= n ? 0 : (int)(n - e0 < DSUB ? n - e0 : DSUB);
   const K* key = reinterpret_cast<const K*>(d.sorted ? d.key[1] : d.key[0]);  // select: a runtime index into the argument copies it to scratch
+  const uint32_t* val = d.sorted ? d.val[1] : d.val[0];
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
-  // the sub-chunk's entries, one per lane (coalesced), then every entry's weighted
-  // feature-gradient row in flight at once
-  const K myk = ch < cnt ? key[e0 + ch] : invalid;
-  const uint32_t ent = ch < cnt ? (d.sorted ? d.val[1] : d.val[0])[e0 + ch] : 0u;
-  const float myw = ch < cnt ? d.w[ent] : 0.f;
+  // the sub-chunk's entries, one per lane (coalesced), and the neighbours' keys
+  const int64_t ec = e0 + ch < n ? e0 + ch : n - 1;
+  const K kraw = key[ec];
+  const uint32_t eraw = val[ec];
+  const K kprev = key[e0 > 0 && e0 <= n ? e0 - 1 : 0];
+  const K knext = key[e0 + cnt < n ? e0 + cnt : 0];
+  const K myk = ch < cnt ? kraw : invalid;
+  const uint32_t ent = myk != invalid ? eraw : 0u;  // an invalid corner (outside the grid, or a
+  const float wraw = d.w[ent];                      // job without a grid gradient: sorted to
+  const float myw = myk != invalid ? wraw : 0.f;    // the end) reads row 0 times weight 0 into
+                                                    // a run that is never written
+  // every entry's feature-gradient row in flight at once, then weighted
   float v[DSUB];
 #pragma unroll
-  for (int i = 0; i < DSUB; ++i) {
-    const uint32_t en = __shfl(ent, i, 32);
-    v[i] = i < cnt ? m.dfeat[(int64_t)(en >> 3) * 32 + ch] * __shfl(myw, i, 32) : 0.f;
-  }
+  for (int i = 0; i < DSUB; ++i) v[i] = m.dfeat[(int64_t)(__shfl(ent, i, 32) >> 3) * 32 + ch];
+#pragma unroll
+  for (int i = 0; i < DSUB; ++i) v[i] = v[i] * __shfl(myw, i, 32);
   int nr = 0;
   if (cnt > 0) {
     K cur = shfl_key(myk, 0);
@@ -153,32 +188,62 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   }
   __syncthreads();
   if (cnt == 0) return;
-  const K prevk = e0 > 0 ? key[e0 - 1] : invalid;
-  const K nextk = e0 + cnt < n ? key[e0 + cnt] : invalid;
+  const K prevk = e0 > 0 ? kprev : invalid;
+  const K nextk = e0 + cnt < n ? knext : invalid;
   float* part = d.part + s * 2 * 32 + ch;
-  // the runs that lie inside the sub-chunk: every destination row read first (all loads in
-  // flight at once), then added to and stored -- one writer per voxel, no atomics
-  float* dst[DSUB];
-  float old[DSUB];
+  const DetRows R = det_rows(m);
+  const uint64_t vmask = (uint64_t(1) << d.vbits) - 1;
+  // the runs that lie inside the sub-chunk, RG at a time: the group's sparse row ids, then
+  // its destination values, read with their loads in flight together, then added to and
+  // stored -- one writer per voxel, no atomics.  (All 32 at once kept 32 pointers and
+  // values live: the compiler put them in scratch, and every reload waited vmcnt(0).)
+  constexpr int RG = 8;
+  for (int r0 = 0; r0 < nr; r0 += RG) {
+    float* dst[RG];
+    if (R.fast) {  // branch-free: the row ids and the destinations are selects
+      int32_t row[RG];
 #pragma unroll
-  for (int r = 0; r < DSUB; ++r) {
-    dst[r] = nullptr;
-    if (r < nr) {
-      const K k = rkey[hw][r];
-      const bool before = r == 0 && prevk == k;
-      const bool cont = r == nr - 1 && nextk == k;
-      if (k != invalid && !before && !cont) dst[r] = det_dst(m, d, (uint64_t)k, ch);
+      for (int u = 0; u < RG; ++u) {
+        const int r = r0 + u < nr ? r0 + u : nr - 1;
+        const K k = rkey[hw][r];
+        const int j = (int)((uint64_t)k >> d.vbits);
+        const int32_t* rows = j == 0 ? R.rows[0] : j == 1 ? R.rows[1] : R.rows[2];
+        row[u] = *(rows ? rows + ((uint64_t)k & vmask) : reinterpret_cast<const int32_t*>(val));
+      }
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const int r = r0 + u < nr ? r0 + u : nr - 1;
+        const K k = rkey[hw][r];
+        const int j = (int)((uint64_t)k >> d.vbits);
+        const int32_t* rows = j == 0 ? R.rows[0] : j == 1 ? R.rows[1] : R.rows[2];
+        float* g = j == 0 ? R.grad[0] : j == 1 ? R.grad[1] : R.grad[2];
+        const int64_t rr = rows ? (int64_t)row[u] : (int64_t)((uint64_t)k & vmask);
+        const bool ok = r0 + u < nr && k != invalid && !(r == 0 && prevk == k) && !(r == nr - 1 && nextk == k) &&
+                        rr >= 0;
+        dst[u] = ok ? g + rr * 32 + ch : nullptr;
+      }
+    } else {  // a strided dense gradient
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const int r = r0 + u < nr ? r0 + u : nr - 1;
+        const K k = rkey[hw][r];
+        const bool ok = r0 + u < nr && k != invalid && !(r == 0 && prevk == k) && !(r == nr - 1 && nextk == k);
+        dst[u] = ok ? det_dst(m, d, (uint64_t)k, ch) : nullptr;
+      }
     }
-    old[r] = dst[r] ? *dst[r] : 0.f;
-  }
+    float old[RG];
 #pragma unroll
-  for (int r = 0; r < DSUB; ++r) {
-    if (r >= nr) break;
-    const K k = rkey[hw][r];
-    if (k == invalid) continue;
-    const float a = racc[hw][r][ch];
-    if (dst[r]) *dst[r] = old[r] + a;
-    else if ((r == 0 && prevk == k) || (r == nr - 1 && nextk == k)) part[r == 0 ? 0 : 32] = a;  // crosses a boundary
+    for (int u = 0; u < RG; ++u) old[u] = *(dst[u] ? dst[u] : d.w);  // d.w[0] when nothing is written
+#pragma unroll
+    for (int u = 0; u < RG; ++u) {
+      const int r = r0 + u;
+      if (r >= nr) break;
+      const K k = rkey[hw][r];
+      if (k == invalid) continue;
+      const float a = racc[hw][r][ch];
+      if (dst[u]) *dst[u] = old[u] + a;
+      else if ((r == 0 && prevk == k) || (r == nr - 1 && nextk == k)) part[r == 0 ? 0 : 32] = a;  // crosses a boundary
+    }
   }
 }
 
