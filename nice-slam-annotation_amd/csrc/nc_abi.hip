@@ -237,6 +237,7 @@ struct Ws {
   int64_t claim_cap = 0;
   bool claims = false;
   int vbits = 0;
+  int dsort_bits = 8;  // NC_DETERMINISTIC radix digit width (det_sort_bits)
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
   bool fuse = false;  // k_mlp_fwd gathers the grid features itself (no k_grid_gather, no feature buffer)
@@ -366,7 +367,8 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
     }
     w.dw = take((size_t)ne * 4);
     w.dpart = take((size_t)(ne + 31) / 32 * 2 * 32 * 4);
-    w.dtemp_bytes = det_sort_temp_bytes(ne, vbits + 2);
+    w.dsort_bits = det_sort_bits(vbits + 2);
+    w.dtemp_bytes = det_sort_temp_bytes(ne, w.dsort_bits);
     w.dtemp = take(w.dtemp_bytes);
   }
   w.total = off;
@@ -466,6 +468,7 @@ DetBufs det_bufs(void* ws, const Ws& w) {
   d.temp = at<void>(ws, w.dtemp);
   d.temp_bytes = w.dtemp_bytes;
   d.vbits = w.vbits;
+  d.sort_bits = w.dsort_bits;
   return d;
 }
 

@@ -291,31 +291,34 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
 //                 inside the wave from 8 ballots, wave offsets through LDS; destination =
 //                 exclusive scan of total[] + hist[d][tile] + rank so far
 // ---------------------------------------------------------------------------
-constexpr int RS_BITS = 8;
-constexpr int RS_BINS = 1 << RS_BITS;
 constexpr int RS_THREADS = 256;
-constexpr int RS_ROUNDS = 16;
+#ifndef NC_RS_ROUNDS
+#define NC_RS_ROUNDS 8  // 2,048-key tiles: 564 workgroups at C2 (16: 282, 5 us slower; 4, 32 slower still)
+#endif
+constexpr int RS_ROUNDS = NC_RS_ROUNDS;
 constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;
+constexpr int RS_MAX_BITS = 11;
 
-template <typename K>
+template <int BITS, typename K>
 __device__ __forceinline__ int rs_digit(K k, int bit) {
-  return (int)((k >> bit) & (K)(RS_BINS - 1));
+  return (int)((k >> bit) & (K)((1 << BITS) - 1));
 }
 
-template <typename K>
+template <int BITS, typename K>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* __restrict__ key, int64_t n, int bit,
                                                         uint32_t* __restrict__ hist, int64_t ntile) {
-  __shared__ uint32_t cnt[RS_BINS];
-  cnt[threadIdx.x] = 0u;
+  constexpr int BINS = 1 << BITS;
+  __shared__ uint32_t cnt[BINS];
+  for (int b = threadIdx.x; b < BINS; b += RS_THREADS) cnt[b] = 0u;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * RS_TILE;
 #pragma unroll 4
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const int64_t e = base + r * RS_THREADS + threadIdx.x;
-    if (e < n) atomicAdd(&cnt[rs_digit(key[e], bit)], 1u);
+    if (e < n) atomicAdd(&cnt[rs_digit<BITS>(key[e], bit)], 1u);
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * ntile + blockIdx.x] = cnt[threadIdx.x];
+  for (int b = threadIdx.x; b < BINS; b += RS_THREADS) hist[(int64_t)b * ntile + blockIdx.x] = cnt[b];
 }
 
 // block-wide exclusive scan of one value per thread (RS_THREADS = 4 waves); returns the
@@ -359,19 +362,29 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scan(uint32_t* __restrict__ h
   if (threadIdx.x == 0) total[blockIdx.x] = all;
 }
 
-template <typename K>
+// BINS = 2^BITS digits, BPT = BINS / RS_THREADS of them per thread (consecutive)
+template <int BITS, typename K>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                            K* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n,
                                                            int bit, const uint32_t* __restrict__ hist, int64_t ntile,
                                                            const uint32_t* __restrict__ total) {
-  __shared__ uint32_t start[RS_BINS];                 // next output slot of each digit for this tile
-  __shared__ uint32_t wcnt[RS_THREADS / 64][RS_BINS];  // this round's count of each digit per wave
+  constexpr int BINS = 1 << BITS, BPT = BINS / RS_THREADS;
+  __shared__ uint32_t start[BINS];                 // next output slot of each digit for this tile
+  __shared__ uint32_t wcnt[RS_THREADS / 64][BINS];  // this round's count of each digit per wave
   __shared__ uint32_t wsum[RS_THREADS / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   {
+    uint32_t t[BPT], sum = 0;
+#pragma unroll
+    for (int q = 0; q < BPT; ++q) sum += (t[q] = total[threadIdx.x * BPT + q]);
     uint32_t all;
-    const uint32_t base = rs_block_exscan(total[threadIdx.x], wsum, &all);
-    start[threadIdx.x] = base + hist[(int64_t)threadIdx.x * ntile + blockIdx.x];
+    uint32_t base = rs_block_exscan(sum, wsum, &all);
+#pragma unroll
+    for (int q = 0; q < BPT; ++q) {
+      const int b = threadIdx.x * BPT + q;
+      start[b] = base + hist[(int64_t)b * ntile + blockIdx.x];
+      base += t[q];
+    }
   }
   const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   const int64_t tile0 = (int64_t)blockIdx.x * RS_TILE;
@@ -379,15 +392,17 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__
     const int64_t e = tile0 + r * RS_THREADS + threadIdx.x;
     if (tile0 + r * RS_THREADS >= n) break;  // block-uniform
 #pragma unroll
-    for (int q = 0; q < RS_THREADS / 64; ++q) wcnt[q][threadIdx.x] = 0u;
+    for (int q = 0; q < RS_THREADS / 64; ++q)
+#pragma unroll
+      for (int c = 0; c < BPT; ++c) wcnt[q][c * RS_THREADS + threadIdx.x] = 0u;
     const bool ok = e < n;
     const K k = ok ? kin[e] : (K)0;
     const uint32_t v = ok ? vin[e] : 0u;
-    const int d = rs_digit(k, bit);
+    const int d = rs_digit<BITS>(k, bit);
     // lanes of this wave holding the same digit (and a valid entry)
     uint64_t same = __ballot(ok);
 #pragma unroll
-    for (int b = 0; b < RS_BITS; ++b) {
+    for (int b = 0; b < BITS; ++b) {
       const uint64_t m = __ballot((d >> b) & 1);
       same &= ((d >> b) & 1) ? m : ~m;
     }
@@ -403,35 +418,52 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__
       vout[off] = v;
     }
     __syncthreads();
-    {
+#pragma unroll
+    for (int c = 0; c < BPT; ++c) {
+      const int b = c * RS_THREADS + threadIdx.x;
       uint32_t add = 0;
 #pragma unroll
-      for (int q = 0; q < RS_THREADS / 64; ++q) add += wcnt[q][threadIdx.x];
-      start[threadIdx.x] += add;
+      for (int q = 0; q < RS_THREADS / 64; ++q) add += wcnt[q][b];
+      start[b] += add;
     }
   }
 }
 
 static int64_t rs_tiles(int64_t n) { return (n + RS_TILE - 1) / RS_TILE; }
 
-size_t det_sort_temp_bytes(int64_t n_entries, int end_bit) {
-  (void)end_bit;
-  return (size_t)(RS_BINS * rs_tiles(n_entries) + RS_BINS) * 4;
+// digit width: the fewest passes over end_bit key bits (at most RS_MAX_BITS per pass), then
+// the narrowest digit that keeps that count -- 20-bit keys (the C2 grids) sort in 2 passes
+// of 10 bits instead of 3 of 8.  NC_DET_SORT_BITS=8..11 pins the width (read when the
+// buffers are laid out; a stable sort has one result, so every width gives bit-identical
+// gradients: test_gpu_determinism checks it)
+int det_sort_bits(int end_bit) {
+  const char* e = std::getenv("NC_DET_SORT_BITS");
+  const int pinned = e ? std::atoi(e) : 0;
+  if (pinned >= 8 && pinned <= RS_MAX_BITS) return pinned;
+  const int passes = (end_bit + RS_MAX_BITS - 1) / RS_MAX_BITS;
+  const int bits = (end_bit + passes - 1) / passes;
+  return bits < 8 ? 8 : bits;
+}
+
+size_t det_sort_temp_bytes(int64_t n_entries, int bits) {
+  const int64_t bins = int64_t(1) << bits;
+  return (size_t)(bins * rs_tiles(n_entries) + bins) * 4;
 }
 
 // sorts (key[0], val[0]) by the low end_bit bits; returns the buffer index holding the result
-template <typename K>
-static int radix_sort(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, int* sorted) {
+template <int BITS, typename K>
+static int radix_sort_w(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, int* sorted) {
+  constexpr int BINS = 1 << BITS;
   const int64_t nt = rs_tiles(n);
   uint32_t* hist = reinterpret_cast<uint32_t*>(d.temp);
-  uint32_t* total = hist + RS_BINS * nt;
+  uint32_t* total = hist + BINS * nt;
   int src = 0;
-  for (int bit = 0; bit < end_bit; bit += RS_BITS) {
+  for (int bit = 0; bit < end_bit; bit += BITS) {
     const K* kin = reinterpret_cast<const K*>(d.key[src]);
     K* kout = reinterpret_cast<K*>(d.key[1 - src]);
-    hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, n, bit, hist, nt);
-    hipLaunchKernelGGL(k_rs_scan, dim3(RS_BINS), dim3(RS_THREADS), 0, s, hist, nt, total);
-    hipLaunchKernelGGL(k_rs_scatter<K>, dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, d.val[src], kout,
+    hipLaunchKernelGGL((k_rs_hist<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, n, bit, hist, nt);
+    hipLaunchKernelGGL(k_rs_scan, dim3(BINS), dim3(RS_THREADS), 0, s, hist, nt, total);
+    hipLaunchKernelGGL((k_rs_scatter<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, d.val[src], kout,
                        d.val[1 - src], n, bit, hist, nt, total);
     if (hipError_t e = hipGetLastError()) return (int)e;
     src = 1 - src;
@@ -441,11 +473,22 @@ static int radix_sort(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, i
 }
 
 template <typename K>
+static int radix_sort(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, int* sorted) {
+  switch (d.sort_bits) {
+    case 8: return radix_sort_w<8, K>(d, n, end_bit, s, sorted);
+    case 9: return radix_sort_w<9, K>(d, n, end_bit, s, sorted);
+    case 10: return radix_sort_w<10, K>(d, n, end_bit, s, sorted);
+    case 11: return radix_sort_w<11, K>(d, n, end_bit, s, sorted);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+template <typename K>
 static int det_scatter(const MlpCtx& m, const DetBufs& d0, int64_t n, hipStream_t s) {
   DetBufs d = d0;
   hipLaunchKernelGGL(k_det_keys<K>, dim3((unsigned)((m.P + 255) / 256), m.n_jobs), dim3(256), 0, s, m, d);
   if (hipError_t e = hipGetLastError()) return (int)e;
-  if (d.temp_bytes < det_sort_temp_bytes(n, d.vbits + 2)) return (int)hipErrorInvalidValue;
+  if (d.temp_bytes < det_sort_temp_bytes(n, d.sort_bits)) return (int)hipErrorInvalidValue;
   if (int e = radix_sort<K>(d, n, d.vbits + 2, s, &d.sorted)) return e;
   const int64_t nsub = (n + DSUB - 1) / DSUB;
   hipLaunchKernelGGL(k_det_runs<K>, dim3((unsigned)((nsub + 7) / 8)), dim3(256), 0, s, m, d, n);

@@ -93,8 +93,10 @@ struct DetBufs {
   size_t temp_bytes;
   int32_t vbits;             // bits of the voxel index; key = job << vbits | voxel
   int32_t sorted;            // which of key[] / val[] holds the sorted entries (set by the sort)
+  int32_t sort_bits;         // radix digit width, fixed with the buffers (det_sort_bits)
 };
-size_t det_sort_temp_bytes(int64_t n_entries, int end_bit);
+int det_sort_bits(int end_bit);
+size_t det_sort_temp_bytes(int64_t n_entries, int bits);
 int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s);
 
 // training-ray sampling (nc_sample.hip)

@@ -150,3 +150,20 @@ def test_deterministic_graph_replay_bitwise(monkeypatch):
                 assert (g0 is None) == (t.grad is None)
                 if g0 is not None:
                     assert torch.equal(t.grad, g0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", ["8", "11"])
+def test_deterministic_sort_digit_width_invariant(bits, monkeypatch):
+    """The radix sort's digit width (default: 2 passes of 10 bits for the room0 grids' 20-bit
+    keys; NC_DET_SORT_BITS pins 8..11) changes the passes, not the result: a stable sort has
+    exactly one output, so the gradients are bit-identical to the default width's."""
+    sc, grids, params, ro, rd, dep = _room0_case(700, "color", seed=5)
+    monkeypatch.delenv("NC_DET_SORT_BITS", raising=False)
+    a = _render_grads(sc, grids, params, ro, rd, dep, "color", True)
+    monkeypatch.setenv("NC_DET_SORT_BITS", bits)
+    b = _render_grads(sc, grids, params, ro, rd, dep, "color", True)
+    assert a.keys() == b.keys() and any(k.startswith("grad/grid") for k in a)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+

@@ -72,6 +72,9 @@ VARIANTS = {
     "scat_u2": ["-DNC_SCAT_UNROLL=2"],
     "scat_u4": ["-DNC_SCAT_UNROLL=4"],
     "scat_u16": ["-DNC_SCAT_UNROLL=16"],
+    "rs_r16": ["-DNC_RS_ROUNDS=16"],  # NC_DETERMINISTIC=1 runs
+    "rs_r4": ["-DNC_RS_ROUNDS=4"],
+    "rs_r32": ["-DNC_RS_ROUNDS=32"],
 }
 # variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
 
