@@ -28,6 +28,24 @@ __device__ __forceinline__ nc_grid grid_of(const MlpCtx& m, int kind) {
 
 // K: uint32_t keys when job and voxel bits fit (vbits + 2 <= 32: every BASELINE grid,
 // C5's 204M-voxel grids included), else uint64_t; the key buffers are sized for 64 bits
+// a point's 8 entries are contiguous: 16-byte stores (the first sort pass takes the entry
+// id from the position, so no id array is written here)
+template <typename T>
+__device__ __forceinline__ void store8(T* dst, const T (&v)[8]) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte entries");
+  if constexpr (sizeof(T) == 4) {
+    uint4* o = reinterpret_cast<uint4*>(dst);
+    o[0] = make_uint4(__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1]),
+                      __builtin_bit_cast(uint32_t, v[2]), __builtin_bit_cast(uint32_t, v[3]));
+    o[1] = make_uint4(__builtin_bit_cast(uint32_t, v[4]), __builtin_bit_cast(uint32_t, v[5]),
+                      __builtin_bit_cast(uint32_t, v[6]), __builtin_bit_cast(uint32_t, v[7]));
+  } else {
+    ulonglong2* o = reinterpret_cast<ulonglong2*>(dst);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = make_ulonglong2(v[2 * q], v[2 * q + 1]);
+  }
+}
+
 template <typename K>
 __global__ void __launch_bounds__(256) k_det_keys(const MlpCtx m, DetBufs d) {
   K* keys = reinterpret_cast<K*>(d.key[0]);
@@ -37,30 +55,32 @@ __global__ void __launch_bounds__(256) k_det_keys(const MlpCtx m, DetBufs d) {
   const Job job = job_of(m, j);
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   const int64_t e0 = ((int64_t)j * m.P + p) * 8;
+  K kk[8];
+  float ww[8];
   if (!job.need_grid) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      keys[e0 + k] = invalid;
-      d.val[0][e0 + k] = (uint32_t)(e0 + k);
-      d.w[e0 + k] = 0.f;
+      kk[k] = invalid;
+      ww[k] = 0.f;
     }
-    return;
-  }
-  const nc_grid G = grid_of(m, job.kind);
-  const float4 n = m.xyz[(int64_t)job.slot * m.P + p];
-  const float xyz[3] = {n.x, n.y, n.z};
-  Corners c;
-  make_corners(G, xyz, c);
-  const uint64_t H = (uint64_t)G.dims[1], W = (uint64_t)G.dims[2];
+  } else {
+    const nc_grid G = grid_of(m, job.kind);
+    const float4 n = m.xyz[(int64_t)job.slot * m.P + p];
+    const float xyz[3] = {n.x, n.y, n.z};
+    Corners c;
+    make_corners(G, xyz, c);
+    const uint64_t H = (uint64_t)G.dims[1], W = (uint64_t)G.dims[2];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint64_t x = (uint64_t)(c.x0 + (k & 1)), y = (uint64_t)(c.y0 + ((k >> 1) & 1)),
-                   z = (uint64_t)(c.z0 + (k >> 2));
-    const bool in = (c.inb >> k) & 1u;
-    keys[e0 + k] = in ? (K)(((uint64_t)j << d.vbits) | ((z * H + y) * W + x)) : invalid;
-    d.val[0][e0 + k] = (uint32_t)(e0 + k);
-    d.w[e0 + k] = c.w[k];
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t x = (uint64_t)(c.x0 + (k & 1)), y = (uint64_t)(c.y0 + ((k >> 1) & 1)),
+                     z = (uint64_t)(c.z0 + (k >> 2));
+      const bool in = (c.inb >> k) & 1u;
+      kk[k] = in ? (K)(((uint64_t)j << d.vbits) | ((z * H + y) * W + x)) : invalid;
+      ww[k] = c.w[k];
+    }
   }
+  store8(keys + e0, kk);
+  store8(d.w + e0, ww);
 }
 
 // The sorted entries are cut into sub-chunks of DSUB = 32, one per half-wave (lane =
@@ -397,7 +417,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__
       for (int c = 0; c < BPT; ++c) wcnt[q][c * RS_THREADS + threadIdx.x] = 0u;
     const bool ok = e < n;
     const K k = ok ? kin[e] : (K)0;
-    const uint32_t v = ok ? vin[e] : 0u;
+    const uint32_t v = ok ? (vin ? vin[e] : (uint32_t)e) : 0u;  // first pass: entry id = position
     const int d = rs_digit<BITS>(k, bit);
     // lanes of this wave holding the same digit (and a valid entry)
     uint64_t same = __ballot(ok);
@@ -450,7 +470,8 @@ size_t det_sort_temp_bytes(int64_t n_entries, int bits) {
   return (size_t)(bins * rs_tiles(n_entries) + bins) * 4;
 }
 
-// sorts (key[0], val[0]) by the low end_bit bits; returns the buffer index holding the result
+// sorts key[0] (with the entry ids, taken from the positions by the first pass) by the low
+// end_bit bits; returns the buffer index holding the result
 template <int BITS, typename K>
 static int radix_sort_w(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, int* sorted) {
   constexpr int BINS = 1 << BITS;
@@ -463,7 +484,8 @@ static int radix_sort_w(const DetBufs& d, int64_t n, int end_bit, hipStream_t s,
     K* kout = reinterpret_cast<K*>(d.key[1 - src]);
     hipLaunchKernelGGL((k_rs_hist<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, n, bit, hist, nt);
     hipLaunchKernelGGL(k_rs_scan, dim3(BINS), dim3(RS_THREADS), 0, s, hist, nt, total);
-    hipLaunchKernelGGL((k_rs_scatter<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, d.val[src], kout,
+    hipLaunchKernelGGL((k_rs_scatter<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin,
+                       bit == 0 ? (const uint32_t*)nullptr : d.val[src], kout,
                        d.val[1 - src], n, bit, hist, nt, total);
     if (hipError_t e = hipGetLastError()) return (int)e;
     src = 1 - src;
