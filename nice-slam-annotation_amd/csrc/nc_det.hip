@@ -134,10 +134,12 @@ struct DetRows {
   float* grad[3];
   const int32_t* rows[3];  // sparse gradient rows, or nullptr: dense channels-last rows
   bool fast;               // every job with a grid gradient has sparse or packed dense rows
+  bool any_rows;           // some job has sparse rows (else no row-id loads at all)
 };
 __device__ __forceinline__ DetRows det_rows(const MlpCtx& m) {
   DetRows r;
   r.fast = true;
+  r.any_rows = false;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const Job job = job_of(m, j);
@@ -148,6 +150,7 @@ __device__ __forceinline__ DetRows det_rows(const MlpCtx& m) {
     const bool packed = G.grad_stride[0] == 1 && G.grad_stride[3] == 32 && G.grad_stride[2] == 32 * W &&
                         G.grad_stride[1] == 32 * W * H;
     r.fast = r.fast && (!job.need_grid || G.grad_rows || packed);
+    r.any_rows = r.any_rows || (job.need_grid && G.grad_rows);
   }
   return r;
 }
@@ -228,7 +231,7 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
         const K k = rkey[hw][r];
         const int j = (int)((uint64_t)k >> d.vbits);
         const int32_t* rows = j == 0 ? R.rows[0] : j == 1 ? R.rows[1] : R.rows[2];
-        row[u] = *(rows ? rows + ((uint64_t)k & vmask) : reinterpret_cast<const int32_t*>(val));
+        row[u] = R.any_rows ? *(rows ? rows + ((uint64_t)k & vmask) : reinterpret_cast<const int32_t*>(val)) : 0;
       }
 #pragma unroll
       for (int u = 0; u < RG; ++u) {
@@ -304,12 +307,14 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
 // seen) or a stale block id whose predecessor never publishes (the look-back spin that
 // was seen).  Both recorded failures are that one mechanism; the sort below has none of
 // it: it is capture-safe by construction, and faster at these sizes.
-//   k_rs_hist     tile of RS_TILE keys per workgroup -> its digit counts, digit-major
-//                 hist[d][tile]
-//   k_rs_scan     one workgroup per digit: exclusive scan of hist[d][*] in place, total[d]
+//   k_rs_hist     tile of RS_TILE keys per workgroup -> its digit counts, tile-major
+//                 hist[tile][d] (one coalesced row per tile; digit-major rows were 4-byte
+//                 writes a tile apart)
+//   k_rs_scan     RS_SCAN_DIG digits per workgroup: exclusive scan of hist[*][d] over the
+//                 tiles in place, total[d]
 //   k_rs_scatter  tile rank by rank: 256 entries per round in input order, stable rank
 //                 inside the wave from 8 ballots, wave offsets through LDS; destination =
-//                 exclusive scan of total[] + hist[d][tile] + rank so far
+//                 exclusive scan of total[] + hist[tile][d] + rank so far
 // ---------------------------------------------------------------------------
 constexpr int RS_THREADS = 256;
 #ifndef NC_RS_ROUNDS
@@ -338,7 +343,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* __restrict__ ke
     if (e < n) atomicAdd(&cnt[rs_digit<BITS>(key[e], bit)], 1u);
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < BINS; b += RS_THREADS) hist[(int64_t)b * ntile + blockIdx.x] = cnt[b];
+  for (int b = threadIdx.x; b < BINS; b += RS_THREADS) hist[(int64_t)blockIdx.x * BINS + b] = cnt[b];
 }
 
 // block-wide exclusive scan of one value per thread (RS_THREADS = 4 waves); returns the
@@ -364,22 +369,41 @@ __device__ __forceinline__ uint32_t rs_block_exscan(uint32_t v, uint32_t* wsum, 
   return before + x - v;
 }
 
+// tile-major counts hist[tile][digit] (the per-tile writes and reads are whole rows): a
+// workgroup scans RS_SCAN_DIG digits, its threads in RS_THREADS / RS_SCAN_DIG groups of
+// consecutive tiles -- the group sums, their exclusive prefix through LDS, then the
+// in-place exclusive scan of each group's range
+#ifndef NC_RS_SCAN_DIG
+#define NC_RS_SCAN_DIG 16
+#endif
+constexpr int RS_SCAN_DIG = NC_RS_SCAN_DIG;
+template <int BITS>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_scan(uint32_t* __restrict__ hist, int64_t ntile,
                                                         uint32_t* __restrict__ total) {
-  __shared__ uint32_t wsum[RS_THREADS / 64];
-  uint32_t* row = hist + (int64_t)blockIdx.x * ntile;
-  const int64_t per = (ntile + RS_THREADS - 1) / RS_THREADS;
-  const int64_t a = threadIdx.x * per, b = a + per < ntile ? a + per : ntile;
-  uint32_t s = 0;
-  for (int64_t i = a; i < b; ++i) s += row[i];
-  uint32_t all;
-  uint32_t run = rs_block_exscan(s, wsum, &all);
-  for (int64_t i = a; i < b; ++i) {
-    const uint32_t c = row[i];
-    row[i] = run;
+  constexpr int BINS = 1 << BITS, TG = RS_THREADS / RS_SCAN_DIG;
+  __shared__ uint32_t part[TG][RS_SCAN_DIG];
+  const int dl = threadIdx.x % RS_SCAN_DIG, g = threadIdx.x / RS_SCAN_DIG;
+  const int b = blockIdx.x * RS_SCAN_DIG + dl;
+  const int64_t per = (ntile + TG - 1) / TG;
+  const int64_t t0 = g * per < ntile ? g * per : ntile, t1 = t0 + per < ntile ? t0 + per : ntile;
+  uint32_t sum = 0;
+#pragma unroll 8
+  for (int64_t t = t0; t < t1; ++t) sum += hist[t * BINS + b];
+  part[g][dl] = sum;
+  __syncthreads();
+  uint32_t run = 0, all = 0;
+#pragma unroll
+  for (int q = 0; q < TG; ++q) {
+    run += q < g ? part[q][dl] : 0u;
+    all += part[q][dl];
+  }
+#pragma unroll 8
+  for (int64_t t = t0; t < t1; ++t) {
+    const uint32_t c = hist[t * BINS + b];
+    hist[t * BINS + b] = run;
     run += c;
   }
-  if (threadIdx.x == 0) total[blockIdx.x] = all;
+  if (g == 0) total[b] = all;
 }
 
 // BINS = 2^BITS digits, BPT = BINS / RS_THREADS of them per thread (consecutive)
@@ -402,7 +426,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__
 #pragma unroll
     for (int q = 0; q < BPT; ++q) {
       const int b = threadIdx.x * BPT + q;
-      start[b] = base + hist[(int64_t)b * ntile + blockIdx.x];
+      start[b] = base + hist[(int64_t)blockIdx.x * BINS + b];
       base += t[q];
     }
   }
@@ -483,7 +507,7 @@ static int radix_sort_w(const DetBufs& d, int64_t n, int end_bit, hipStream_t s,
     const K* kin = reinterpret_cast<const K*>(d.key[src]);
     K* kout = reinterpret_cast<K*>(d.key[1 - src]);
     hipLaunchKernelGGL((k_rs_hist<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, n, bit, hist, nt);
-    hipLaunchKernelGGL(k_rs_scan, dim3(BINS), dim3(RS_THREADS), 0, s, hist, nt, total);
+    hipLaunchKernelGGL(k_rs_scan<BITS>, dim3(BINS / RS_SCAN_DIG), dim3(RS_THREADS), 0, s, hist, nt, total);
     hipLaunchKernelGGL((k_rs_scatter<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin,
                        bit == 0 ? (const uint32_t*)nullptr : d.val[src], kout,
                        d.val[1 - src], n, bit, hist, nt, total);

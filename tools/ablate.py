@@ -75,6 +75,9 @@ VARIANTS = {
     "rs_r16": ["-DNC_RS_ROUNDS=16"],  # NC_DETERMINISTIC=1 runs
     "rs_r4": ["-DNC_RS_ROUNDS=4"],
     "rs_r32": ["-DNC_RS_ROUNDS=32"],
+    "scan_d8": ["-DNC_RS_SCAN_DIG=8"],
+    "scan_d4": ["-DNC_RS_SCAN_DIG=4"],
+    "scan_d32": ["-DNC_RS_SCAN_DIG=32"],
 }
 # variants built by hand (source edits) are run by name if dbg/abl_<name>.so exists
 
