@@ -121,11 +121,6 @@ __device__ __forceinline__ float* det_dst(const MlpCtx& m, const DetBufs& d, uin
   return G.grad + z * G.grad_stride[1] + y * G.grad_stride[2] + x * G.grad_stride[3] + (int64_t)ch * G.grad_stride[0];
 }
 
-__device__ __forceinline__ void det_add(const MlpCtx& m, const DetBufs& d, uint64_t k0, int ch, float acc) {
-  float* dst = det_dst(m, d, k0, ch);
-  if (dst) *dst = *dst + acc;
-}
-
 // The gradient row of voxel key k0 resolved through per-job descriptors read once per
 // launch (job and grid are uniform there, so they sit in scalar registers): the run loop
 // then selects among them per run instead of indexing the kernel argument with a
@@ -270,7 +265,11 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   }
 }
 
-// half-wave = sub-chunk s: if a run starts in s and continues past it, sum its pieces
+// half-wave = sub-chunk s: if a run starts in s and continues past it, sum its pieces.
+// The four neighbour keys are read together and the following sub-chunks' pieces and end
+// keys JOIN_AHEAD at a time (clamped, unconditional loads); the pieces are still added one
+// by one in sub-chunk order
+constexpr int JOIN_AHEAD = 4;
 template <typename K>
 __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int64_t n) {
   const int64_t s = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
@@ -278,19 +277,52 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
   const int64_t e0 = s * DSUB;
   if (e0 >= n) return;
   const int64_t e1 = e0 + DSUB < n ? e0 + DSUB : n;
+  const int64_t nsub = (n + DSUB - 1) / DSUB;
   const K* key = reinterpret_cast<const K*>(d.sorted ? d.key[1] : d.key[0]);  // select: a runtime index into the argument copies it to scratch
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   const K last = key[e1 - 1];
-  if (last == invalid || e1 >= n || key[e1] != last) return;  // no run continues past s
-  const bool single = key[e0] == last;
-  if (single && e0 > 0 && key[e0 - 1] == last) return;  // it started before s: not the owner
+  const K after = key[e1 < n ? e1 : e1 - 1];
+  const K first = key[e0];
+  const K before = key[e0 > 0 ? e0 - 1 : e0];
+  // (non-short-circuit: all four loads are used before the one exit, so none is sunk past it)
+  const bool cont = (last != invalid) & (e1 < n) & (after == last);  // a run continues past s
+  const bool single = first == last;
+  if (!(cont & !(single & (e0 > 0) & (before == last)))) return;  // or it started before s: not the owner
   float acc = d.part[(s * 2 + (single ? 0 : 1)) * 32 + ch];
-  for (int64_t t = s + 1;; ++t) {
-    acc = acc + d.part[t * 2 * 32 + ch];
-    const int64_t te = (t + 1) * DSUB;
-    if (te >= n || key[te] != last) break;  // the run ends inside t (or at its end)
+  for (int64_t t = s + 1;; t += JOIN_AHEAD) {
+    float pv[JOIN_AHEAD];
+    K kv[JOIN_AHEAD];
+#pragma unroll
+    for (int u = 0; u < JOIN_AHEAD; ++u) {
+      const int64_t tt = t + u < nsub ? t + u : nsub - 1;
+      const int64_t te = (tt + 1) * DSUB;
+      pv[u] = d.part[tt * 2 * 32 + ch];
+      kv[u] = key[te < n ? te : n - 1];
+    }
+    bool done = false;
+#pragma unroll
+    for (int u = 0; u < JOIN_AHEAD; ++u) {
+      if (!done) {
+        acc = acc + pv[u];
+        const int64_t te = (t + u + 1) * DSUB;
+        done = te >= n || kv[u] != last;  // the run ends inside t + u (or at its end)
+      }
+    }
+    if (done) break;
   }
-  det_add(m, d, last, ch, acc);
+  const DetRows R = det_rows(m);
+  float* dst;
+  if (R.fast) {
+    const int j = (int)((uint64_t)last >> d.vbits);
+    const uint64_t v = (uint64_t)last & ((uint64_t(1) << d.vbits) - 1);
+    const int32_t* rows = j == 0 ? R.rows[0] : j == 1 ? R.rows[1] : R.rows[2];
+    float* g = j == 0 ? R.grad[0] : j == 1 ? R.grad[1] : R.grad[2];
+    const int64_t rr = rows ? (int64_t)rows[v] : (int64_t)v;
+    dst = rr >= 0 ? g + rr * 32 + ch : nullptr;
+  } else {
+    dst = det_dst(m, d, (uint64_t)last, ch);
+  }
+  if (dst) *dst = *dst + acc;
 }
 
 // ---------------------------------------------------------------------------

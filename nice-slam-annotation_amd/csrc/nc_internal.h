@@ -193,7 +193,12 @@ struct RayCtx {
 int64_t fused_loss_blocks(int64_t N);
 
 // ray r is kept (nc_render_args.ray_valid)
-__device__ __forceinline__ bool ray_ok(const RayCtx& c, int64_t r) { return c.valid == nullptr || c.valid[r] != 0; }
+// (the flag byte is loaded unconditionally -- from the workspace's sample depths when there
+// is no mask -- so the load is not sunk into a branch of its own and waited for alone)
+__device__ __forceinline__ bool ray_ok(const RayCtx& c, int64_t r) {
+  const uint8_t f = *(c.valid ? c.valid + r : reinterpret_cast<const uint8_t*>(c.z));
+  return c.valid == nullptr || f != 0;
+}
 
 // One layer GEMM of the iMAP* MLP (nc_imap.hip): C[m][n] (+)= sum_k A(m,k) B(k,n)
 struct ImapGemm {

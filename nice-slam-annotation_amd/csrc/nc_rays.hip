@@ -73,14 +73,36 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
     d[k] = (double)c.rays_d[rr * 3 + k];
   }
   const float gd_in = (c.gt_depth && c.N > 0) ? c.gt_depth[rr] : 0.f;
+  // the per-lane sample inputs too (clamped indices, used below by lane range): a load
+  // under a branch of its only use is issued alone and waited for
+  const float t_str = c.t_strat[lane < c.n_strat ? lane : 0];
+  const double t_srf = c.n_surf > 0 ? c.t_surf[lane >= c.n_strat && lane < c.n_strat + c.n_surf ? lane - c.n_strat : 0] : 0.0;
+  const int xl = lane - c.n_strat - c.n_surf;
+  const double z_ex = c.n_extra > 0 ? c.z_extra[rr * c.n_extra + (xl >= 0 && xl < c.n_extra ? xl : 0)] : 0.0;
+  const float t_rnd = c.t_rand ? c.t_rand[rr * c.n_strat + (lane < c.n_strat ? lane : 0)] : 0.f;
+  const float dmax_arg = *(c.depth_max ? c.depth_max : reinterpret_cast<const float*>(c.z));  // when !dmax_local
+  const bool ok = ray_ok(c, rr);  // a dropped ray's samples stay finite: they feed the decoders
   float dmax_blk = 0.f;
   if (c.dmax_local) {  // torch.max(gt_depth) over the whole batch, by every workgroup (N small)
     __shared__ float red[RAY_WAVES];
     float m = -INFINITY;
-    for (int64_t k = threadIdx.x; k < c.N; k += blockDim.x) {
-      if (c.valid && !c.valid[k]) continue;  // dropped rays (ray_valid) are not in the batch
-      const float v = c.gt_depth[k];
-      m = (v > m || isnan(v)) ? v : m;
+    // 4 strides at a time, every load unconditional (clamped index; without a mask the
+    // flag byte is read from the depths and ignored) so all 8 are in flight together
+    constexpr int U = 4;
+    for (int64_t k0 = threadIdx.x; k0 < c.N; k0 += U * blockDim.x) {
+      float v[U];
+      uint8_t f[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t k = k0 + u * blockDim.x < c.N ? k0 + u * blockDim.x : c.N - 1;
+        v[u] = c.gt_depth[k];
+        f[u] = *(c.valid ? c.valid + k : reinterpret_cast<const uint8_t*>(c.gt_depth));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // in k order; dropped rays (ray_valid) are not in the batch
+        const bool keep = k0 + u * blockDim.x < c.N && (!c.valid || f[u]);
+        m = keep && (v[u] > m || isnan(v[u])) ? v[u] : m;
+      }
     }
     for (int o = 32; o > 0; o >>= 1) {
       const float v = __shfl_xor(m, o);
@@ -108,14 +130,14 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
   float gd = 0.f, dmax = 0.f;
   if (has_depth) {
     gd = gd_in;
-    dmax = c.dmax_local ? dmax_blk : *c.depth_max;
+    dmax = c.dmax_local ? dmax_blk : dmax_arg;
     const double hi = (double)(dmax * 1.2f);  // torch.max(gt_depth*1.2) (float32)
     double v = far_bb < 0.0 ? 0.0 : far_bb;   // torch.clamp(far_bb, 0, hi)
     far = v > hi ? hi : v;
   }
   double z;
   if (lane < c.n_strat) {
-    const float t = c.t_strat[lane];
+    const float t = t_str;
     const float om = 1.0f - t;                               // (1.-t_vals)
     if (!c.lindisp) {
       const float nearw = has_depth ? (gd * 0.01f) * om : 0.01f * om;  // near*(1-t), float32
@@ -125,14 +147,14 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
       z = 1.0 / ((double)(inv_near * om) + (1.0 / far) * (double)t);
     }
   } else if (lane < c.n_strat + c.n_surf) {
-    const double ts = c.t_surf[lane - c.n_strat];
+    const double ts = t_srf;
     if (gd > 0.f) {  // Renderer.py:185-187
       z = (double)(0.95f * gd) * (1.0 - ts) + (double)(1.05f * gd) * ts;
     } else {         // Renderer.py:193-196
       z = 0.001 * (1.0 - ts) + (double)dmax * ts;
     }
   } else if (lane < c.S) {  // importance samples (Renderer.py:248: sorted with the rest)
-    z = c.z_extra[r * c.n_extra + (lane - c.n_strat - c.n_surf)];
+    z = z_ex;
   } else {
     z = INFINITY;
   }
@@ -141,7 +163,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
     if (lane < c.n_strat) {
       const double lower = lane > 0 ? .5 * (z + zp) : z;
       const double upper = lane < c.n_strat - 1 ? .5 * (zn + z) : z;
-      z = lower + (upper - lower) * (double)c.t_rand[r * c.n_strat + lane];
+      z = lower + (upper - lower) * (double)t_rnd;
     }
   }
 #ifdef NC_ABL_NO_SORT  // timing-only ablation: samples left unsorted
@@ -162,7 +184,6 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
       }
     }
   }
-  const bool ok = ray_ok(c, r);  // a dropped ray's samples stay finite: they feed the decoders
   if (!ok && !isfinite(z)) z = 0.0;
   if (lane < c.S) {
     const int64_t p = r * c.S + lane;
@@ -203,9 +224,11 @@ __global__ void k_points_prep(const MlpCtx m, float4* xyz, float4* pf) {
 }
 
 // strict in-bound mask of Renderer.py:63-66 against the renderer bound
+// (the three coordinates loaded first and the tests combined without short-circuit: with
+// && each later load sits in a branch of its own and is waited for alone)
 __device__ __forceinline__ bool in_bound(const double* p, const double (&b)[3][2]) {
-  return p[0] < b[0][1] && p[0] > b[0][0] && p[1] < b[1][1] && p[1] > b[1][0] && p[2] < b[2][1] &&
-         p[2] > b[2][0];
+  const double x = p[0], y = p[1], z = p[2];
+  return (x < b[0][1]) & (x > b[0][0]) & (y < b[1][1]) & (y > b[1][0]) & (z < b[2][1]) & (z > b[2][0]);
 }
 
 struct SampleState {
@@ -220,14 +243,25 @@ struct SampleState {
 __device__ __forceinline__ void sample_state(const RayCtx& c, int64_t r, int lane, SampleState& s) {
   const bool act = lane < c.S;
   const int64_t p = r * c.S + (act ? lane : 0);
-  s.z = act ? c.z[p] : 0.0;
-  float occ = 0.f;
-  if (c.occ_a >= 0) occ = c.occ[(int64_t)c.occ_a * c.P + p];
-  if (c.occ_b >= 0) occ = occ + c.occ[(int64_t)c.occ_b * c.P + p];  // fine_occ + middle_occ
+  const double zl = c.z[p];  // p is clamped: loaded unconditionally, then selected
+  s.z = act ? zl : 0.0;
+  // every per-sample load of the state unconditional, so they issue together (a load under
+  // a branch, even a uniform one, is waited for before the loads after the branch)
+  const float* ob = c.occ ? c.occ : reinterpret_cast<const float*>(c.z);
+  const float oa = ob[(int64_t)(c.occ_a >= 0 ? c.occ_a : 0) * c.P + p];
+  const float obv = ob[(int64_t)(c.occ_b >= 0 ? c.occ_b : 0) * c.P + p];
+  const float occ_a = c.occ_a >= 0 ? oa : 0.f;
+  const float occ_ab = occ_a + obv;  // fine_occ + middle_occ (formed always: a select, not a branch)
+  float occ = c.occ_b >= 0 ? occ_ab : occ_a;
   s.inb = in_bound(c.pts + p * 3, c.bound);
   if (!s.inb) occ = 100.f;  // Renderer.py:87
+  // colour loaded unconditionally too (from the sample depths when there is none)
+  const float* rp = c.has_rgb ? c.rgb + p * 3 : reinterpret_cast<const float*>(c.z + p);
+  float rv[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) s.rgb[k] = c.has_rgb ? c.rgb[p * 3 + k] : 0.f;
+  for (int k = 0; k < 3; ++k) rv[k] = rp[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.rgb[k] = c.has_rgb ? rv[k] : 0.f;
   if (c.density) {  // iMAP*: raw2alpha(raw, dists) = 1 - exp(-relu(raw) * dists) (common.py:232-247)
     const double zn = __shfl_down(s.z, 1);
     s.dist = (lane + 1 < c.S) ? (float)(zn - s.z) : 1e10f;  // dists.float(), 1e10 after the last sample
@@ -593,25 +627,30 @@ __global__ void __launch_bounds__(64 * FUSED_RAYS) k_composite_fwd_loss(const Ra
   const bool col_term = (c.loss_flags & NC_LOSS_COLOR) != 0;
   double ld = 0.0, lc = 0.0;
   if (r < c.N) {
+    // the loss targets and the ray flag first, with unconditional uses (a load used only
+    // in a branch is sunk into it and waited for there, after the compositing)
+    const bool ok = ray_ok(c, r);  // a dropped ray (ray_valid) is not in the loss
+    const float gt = c.loss_depth[r];
+    const float* tcp = col_term ? c.loss_color + r * 3 : c.loss_depth + r;
+    float tc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tc[k] = tcp[col_term ? k : 0];
     SampleState s;
     sample_state(c, r, lane, s);
     double depth;
     float col[3];
     composite_fwd_ray(c, r, lane, s, depth, col);
-    const bool ok = ray_ok(c, r);  // a dropped ray (ray_valid) is not in the loss
-    const float gt = c.loss_depth[r];
     const bool m = ok && gt > 0.f;
     const double diff = (double)gt - depth;
     const double coef = m ? -sgn_d(diff) : 0.0;
     ld = m ? fabs(diff) : 0.0;
-    float gC[3] = {0.f, 0.f, 0.f};
-    if (col_term && ok) {
+    float gC[3];
+    const bool use_c = col_term && ok;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float dc = c.loss_color[r * 3 + k] - col[k];
-        lc += (double)fabsf(dc);  // the mapper's colour term is unmasked
-        gC[k] = -(c.w_color * sgn_f(dc));
-      }
+    for (int k = 0; k < 3; ++k) {
+      const float dc = tc[k] - col[k];
+      lc += use_c ? (double)fabsf(dc) : 0.0;  // the mapper's colour term is unmasked
+      gC[k] = use_c ? -(c.w_color * sgn_f(dc)) : 0.f;
     }
     if (lane == 0) {
       c.coef_d[r] = coef;
@@ -675,14 +714,25 @@ __device__ __forceinline__ void ray_grads_body(const RayCtx& c, int64_t block) {
   if (r >= c.N) return;
   const bool act = lane < c.S && ray_ok(c, r);  // a dropped ray's gradients are 0
   const int64_t p = r * c.S + (lane < c.S ? lane : 0);
-  double dp[3] = {0.0, 0.0, 0.0};
-  if (act) {
-    for (int j = 0; j < c.n_jobs; ++j) {
+  // every job's point gradient and the depth loaded unconditionally (clamped), then summed
+  // in job order and selected: no load waits alone in a branch
+  double g[MAX_JOBS][3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) dp[k] += c.dpts[((int64_t)j * c.P + p) * 3 + k];
-    }
+  for (int j = 0; j < MAX_JOBS; ++j) {
+    const int jj = j < c.n_jobs ? j : 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[j][k] = c.dpts[((int64_t)jj * c.P + p) * 3 + k];
   }
-  const double z = act ? c.z[p] : 0.0;
+  const double zl = c.z[p];
+  double dp[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < MAX_JOBS; ++j) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dp[k] = j < c.n_jobs ? dp[k] + g[j][k] : dp[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) dp[k] = act ? dp[k] : 0.0;
+  const double z = act ? zl : 0.0;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const double go = wsum_d(dp[k]);
