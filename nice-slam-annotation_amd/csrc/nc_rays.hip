@@ -757,6 +757,10 @@ __global__ void __launch_bounds__(256) k_ray_grads(const RayCtx c) { ray_grads_b
 // thread = (float4 column of the parameter vector, part): part p sums slab rows
 // p, p+8, ... (independent loads in flight), the 8 partial sums meet in LDS.
 constexpr int PR_COLS = 32, PR_PARTS = 8;
+#ifndef NC_PR_AHEAD
+#define NC_PR_AHEAD 4
+#endif
+constexpr int PR_AHEAD = NC_PR_AHEAD;  // slab rows in flight per thread (8 / 12: no gain, profiles/r04/ray_loads/ab_pr.log)
 static_assert(PR_COLS * PR_PARTS == 64 * RAY_WAVES, "k_param_ray_reduce: one block size for both roles");
 __device__ __forceinline__ void param_reduce_body(const ParamReduceCtx& c, int bx, int j) {
   __shared__ float4 part[PR_PARTS][PR_COLS];
@@ -776,13 +780,15 @@ __device__ __forceinline__ void param_reduce_body(const ParamReduceCtx& c, int b
     auto row = [&](int w) { return *reinterpret_cast<const float4*>(src + (int64_t)w * c.slab_stride); };
     const int nw = w1 - w0;
     int w = prt;
-    // four rows in flight, added in the same order as one at a time (bit-identical sums)
-    for (; w + 3 * PR_PARTS < nw; w += 4 * PR_PARTS) {
-      const float4 v0 = row(w), v1 = row(w + PR_PARTS), v2 = row(w + 2 * PR_PARTS), v3 = row(w + 3 * PR_PARTS);
-      acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
-      acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
-      acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
-      acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
+    // PR_AHEAD rows in flight, added in the same order as one at a time (bit-identical sums)
+    for (; w + (PR_AHEAD - 1) * PR_PARTS < nw; w += PR_AHEAD * PR_PARTS) {
+      float4 v[PR_AHEAD];
+#pragma unroll
+      for (int u = 0; u < PR_AHEAD; ++u) v[u] = row(w + u * PR_PARTS);
+#pragma unroll
+      for (int u = 0; u < PR_AHEAD; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
     }
     for (; w < nw; w += PR_PARTS) {
       const float4 v = row(w);
