@@ -482,9 +482,11 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
     }
     if (cached) {
       for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
+        const bool okr = ray_ok(c, r);
         double diff, s;
         const double t = tracker_tmp(c, r, diff, s);
-        skey[r] = !ray_ok(c, r) ? KEY_DROPPED : isnan(t) ? ~0ull : (unsigned long long)__double_as_longlong(t);
+        const unsigned long long kt = isnan(t) ? ~0ull : (unsigned long long)__double_as_longlong(t);
+        skey[r] = okr ? kt : KEY_DROPPED;  // a select: the flag and the inputs load together
       }
     }
     unsigned long long pmask = 0ull;
@@ -543,37 +545,44 @@ __global__ void __launch_bounds__(LOSS_THREADS) k_loss(const RayCtx c) {
   }
   double sd = 0.0, sc = 0.0;
   for (int64_t r = tid; r < c.N; r += LOSS_THREADS) {
-    if (!ray_ok(c, r)) {  // a dropped ray (ray_valid) is not in the loss
-      c.coef_d[r] = 0.0;
-      if (col) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) c.coef_c[r * 3 + k] = 0.f;
-      }
-      continue;
-    }
+    // the ray's inputs loaded first, unconditionally (a load under a branch waits alone);
+    // a dropped ray (ray_valid) is masked out of both terms and gets zero coefficients
+    const bool ok = ray_ok(c, r);
     const float gt = c.loss_depth[r];
-    bool m = gt > 0.f;
+    const double dep = c.depth[r];
+    const double vr = c.var[r];
+    const float* lcp = col ? c.loss_color + r * 3 : c.loss_depth + r;
+    float lc[3], cc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      lc[k] = lcp[col ? k : 0];
+      cc[k] = c.color[r * 3 + k];
+    }
+    bool m = ok && gt > 0.f;
     double val, coef;
-    if (tracker) {
-      double diff, s;
-      val = tracker_tmp(c, r, diff, s);
+    const double diff = (double)gt - dep;
+    if (tracker) {  // tracker_tmp
+      const double sdev = sqrt(vr + 1e-10);
+      val = fabs(diff) / sdev;
       if (dyn) m = m && (val < thr);
-      coef = -(sgn_d(diff) * (1.0 / s));
+      coef = -(sgn_d(diff) * (1.0 / sdev));
     } else {
-      const double diff = (double)gt - c.depth[r];
       val = fabs(diff);
       coef = -sgn_d(diff);
     }
-    if (m) sd += val;
+    sd = m ? sd + val : sd;
     c.coef_d[r] = m ? coef : 0.0;
     if (col) {
-      const bool mc = tracker ? m : true;  // the mapper's colour term is unmasked
+      const bool mc = ok && (tracker ? m : true);  // the mapper's colour term is unmasked
+      float cf[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const float dc = c.loss_color[r * 3 + k] - c.color[r * 3 + k];
-        if (mc) sc += (double)fabsf(dc);
-        c.coef_c[r * 3 + k] = mc ? -(c.w_color * sgn_f(dc)) : 0.f;
+        const float dc = lc[k] - cc[k];
+        sc = mc ? sc + (double)fabsf(dc) : sc;
+        cf[k] = mc ? -(c.w_color * sgn_f(dc)) : 0.f;
       }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) c.coef_c[r * 3 + k] = cf[k];
     }
   }
   sd = wsum_d(sd);
