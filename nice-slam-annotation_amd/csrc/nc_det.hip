@@ -464,6 +464,26 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__
   }
   const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   const int64_t tile0 = (int64_t)blockIdx.x * RS_TILE;
+  // the whole tile's keys and ids loaded up front (clamped, all in flight together), the
+  // rounds then run from registers
+  K kt[RS_ROUNDS];
+  uint32_t vt[RS_ROUNDS];
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int64_t e = tile0 + r * RS_THREADS + threadIdx.x;
+    kt[r] = kin[e < n ? e : n - 1];
+  }
+  if (vin) {
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+      const int64_t e = tile0 + r * RS_THREADS + threadIdx.x;
+      vt[r] = vin[e < n ? e : n - 1];
+    }
+  } else {  // first pass: entry id = position
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) vt[r] = (uint32_t)(tile0 + r * RS_THREADS + threadIdx.x);
+  }
+#pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const int64_t e = tile0 + r * RS_THREADS + threadIdx.x;
     if (tile0 + r * RS_THREADS >= n) break;  // block-uniform
@@ -472,8 +492,8 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* __restrict__
 #pragma unroll
       for (int c = 0; c < BPT; ++c) wcnt[q][c * RS_THREADS + threadIdx.x] = 0u;
     const bool ok = e < n;
-    const K k = ok ? kin[e] : (K)0;
-    const uint32_t v = ok ? (vin ? vin[e] : (uint32_t)e) : 0u;  // first pass: entry id = position
+    const K k = ok ? kt[r] : (K)0;
+    const uint32_t v = ok ? vt[r] : 0u;
     const int d = rs_digit<BITS>(k, bit);
     // lanes of this wave holding the same digit (and a valid entry)
     uint64_t same = __ballot(ok);
