@@ -215,7 +215,10 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   // its destination values, read with their loads in flight together, then added to and
   // stored -- one writer per voxel, no atomics.  (All 32 at once kept 32 pointers and
   // values live: the compiler put them in scratch, and every reload waited vmcnt(0).)
-  constexpr int RG = 8;
+#ifndef NC_DET_RG
+#define NC_DET_RG 8
+#endif
+  constexpr int RG = NC_DET_RG;
   for (int r0 = 0; r0 < nr; r0 += RG) {
     float* dst[RG];
     if (R.fast) {  // branch-free: the row ids and the destinations are selects
