@@ -412,6 +412,7 @@ __device__ __forceinline__ uint32_t rs_block_exscan(uint32_t v, uint32_t* wsum, 
 #define NC_RS_SCAN_DIG 16
 #endif
 constexpr int RS_SCAN_DIG = NC_RS_SCAN_DIG;
+constexpr int RS_SCAN_REG = 48;  // tiles per thread held in registers (C2: 36); more: two passes over memory
 template <int BITS>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_scan(uint32_t* __restrict__ hist, int64_t ntile,
                                                         uint32_t* __restrict__ total) {
@@ -422,6 +423,31 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scan(uint32_t* __restrict__ h
   const int64_t per = (ntile + TG - 1) / TG;
   const int64_t t0 = g * per < ntile ? g * per : ntile, t1 = t0 + per < ntile ? t0 + per : ntile;
   uint32_t sum = 0;
+  if (per <= RS_SCAN_REG) {  // the group's counts held in registers between the two passes,
+    uint32_t cv[RS_SCAN_REG];  // loaded together (clamped, unconditional)
+#pragma unroll
+    for (int i = 0; i < RS_SCAN_REG; ++i) {
+      const int64_t t = t0 + i < t1 ? t0 + i : (t1 > 0 ? t1 - 1 : 0);
+      cv[i] = hist[t * BINS + b];
+    }
+#pragma unroll
+    for (int i = 0; i < RS_SCAN_REG; ++i) sum += t0 + i < t1 ? cv[i] : 0u;
+    part[g][dl] = sum;
+    __syncthreads();
+    uint32_t run = 0, all = 0;
+#pragma unroll
+    for (int q = 0; q < TG; ++q) {
+      run += q < g ? part[q][dl] : 0u;
+      all += part[q][dl];
+    }
+#pragma unroll
+    for (int i = 0; i < RS_SCAN_REG; ++i) {
+      if (t0 + i < t1) hist[(t0 + i) * BINS + b] = run;
+      run += t0 + i < t1 ? cv[i] : 0u;
+    }
+    if (g == 0) total[b] = all;
+    return;
+  }
 #pragma unroll 8
   for (int64_t t = t0; t < t1; ++t) sum += hist[t * BINS + b];
   part[g][dl] = sum;
