@@ -105,6 +105,10 @@ def parse():
                     help="draw ONE batch of N x --rays rays (seed 1000) and give rank r its contiguous shard "
                          "(distributed.shard), instead of --rays fresh rays per rank: the N-rank step then "
                          "computes the gradients of the 1-rank step over the whole batch (tests)")
+    ap.add_argument("--global-rays", type=int, default=0,
+                    help="one batch of this many rays in total (seed 1000), rank r rendering its contiguous "
+                         "shard (distributed.shard_bounds: the first total %% N ranks get one ray more); "
+                         "--rays is then the shard size (tests: uneven shards)")
     ap.add_argument("--dump-grads", default=None,
                     help="after the timed steps run one more step and have rank 0 save its exchanged "
                          "gradients (decoder parameters; grid rows of the frustum, or whole grids without "
@@ -206,7 +210,11 @@ def build_workload(args, rank, device, world=1):
     for n in ("middle", "fine", "color"):
         getattr(model, n + "_decoder").bound = model.bound
     model.coarse_decoder.bound = (sc.bound * 2).to(device)
-    if getattr(args, "global_batch", False):  # one batch over all ranks, contiguous shards
+    if getattr(args, "global_rays", 0):  # one batch of a given total, possibly uneven shards
+        from nicecore.distributed import shard
+        ro, rd, dep, col = shard(rank, world, *S.synth_rays(sc, args.global_rays, seed=1000))
+        args.rays = int(ro.shape[0])
+    elif getattr(args, "global_batch", False):  # one batch over all ranks, contiguous shards
         from nicecore.distributed import shard
         ro, rd, dep, col = shard(rank, world, *S.synth_rays(sc, args.rays * world, seed=1000))
     else:
@@ -354,6 +362,7 @@ def make_step(w, args, world, device):
                 pre()
                 g()
                 split_post(g2)
+        graphed.step = g  # its .out: the loss of the last replay (tests score the replayed step)
     return eager, graphed
 
 
@@ -664,7 +673,8 @@ def main():
                 "timing": timing_src}
     peak_rays, f_ray, b_ray = step_roofline_rays_s(args.stage, S, args.mode, args.fix_fine)
 
-    value = world * args.rays * args.steps / dt
+    total_rays = args.global_rays or world * args.rays  # rays all ranks render per step
+    value = total_rays * args.steps / dt
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 4),
@@ -700,7 +710,7 @@ def main():
         eager()  # one more step: render + loss + backward + the gradient exchange
         torch.cuda.synchronize()
         if rank == 0:
-            dump = {"world": world, "rays_per_rank": args.rays,
+            dump = {"world": world, "rays_per_rank": args.rays, "total_rays": total_rays,
                     "params": {n: p.grad.detach().cpu() for n, p in w["model"].named_parameters()
                                if p.grad is not None}, "grids": {}}
             for k, g in w["grids"].items():

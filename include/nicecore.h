@@ -453,6 +453,11 @@ int nc_adam_step_multi(const nc_adam_args* args, const nc_adam_segment* segments
 int nc_abi_version(void);
 const char* nc_last_error(void);
 
+/* The sources this binary was compiled from: the first 16 hex digits of a sha256 over
+ * csrc/ and this header (nicecore/build.py:source_hash, passed as -DNC_SRC_HASH).  The
+ * Python binding refuses a library whose id differs from the tree it is loaded from. */
+const char* nc_build_id(void);
+
 /* Number of floats in a decoder's flat parameter vector (58,956 over all four). */
 int64_t nc_param_count(int decoder);
 

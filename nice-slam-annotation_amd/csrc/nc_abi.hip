@@ -723,6 +723,13 @@ extern "C" {
 
 int nc_abi_version(void) { return NC_ABI_VERSION; }
 
+#ifndef NC_SRC_HASH
+#define NC_SRC_HASH "unknown-source00"
+#endif
+// "nicecore-src-<hash>" is also found in the file's bytes (build.py:library_build_id)
+static const char kBuildTag[] = "nicecore-src-" NC_SRC_HASH;
+const char* nc_build_id(void) { return kBuildTag + 13; }
+
 const char* nc_last_error(void) { return g_err.c_str(); }
 
 int64_t nc_param_count(int decoder) { return nparam_of(decoder); }

@@ -229,7 +229,10 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
         const K k = rkey[hw][r];
         const int j = (int)((uint64_t)k >> d.vbits);
         const int32_t* rows = j == 0 ? R.rows[0] : j == 1 ? R.rows[1] : R.rows[2];
-        row[u] = R.any_rows ? *(rows ? rows + ((uint64_t)k & vmask) : reinterpret_cast<const int32_t*>(val)) : 0;
+        // the invalid key (all ones: j = 3, voxel 2^vbits - 1) is in every sort's tail; its
+        // voxel index lies at or past the end of job 2's [D*H*W] row map, so it reads val[0]
+        const bool live = rows != nullptr && k != invalid;
+        row[u] = R.any_rows ? *(live ? rows + ((uint64_t)k & vmask) : reinterpret_cast<const int32_t*>(val)) : 0;
       }
 #pragma unroll
       for (int u = 0; u < RG; ++u) {

@@ -163,6 +163,7 @@ NC_ADAM_SPARSE_ROWS = 1
 EXPORTS = {
     "nc_abi_version": (c_int, []),
     "nc_last_error": (ctypes.c_char_p, []),
+    "nc_build_id": (ctypes.c_char_p, []),
     "nc_param_count": (c_int64, [c_int]),
     "nc_struct_size": (c_size_t, [c_int]),
     "nc_render_workspace_bytes": (c_size_t, [POINTER(NcRenderArgs)]),
@@ -210,6 +211,8 @@ def load(path: str | None = None):
     if _lib is not None:
         return _lib
     p = path or os.environ.get("NICECORE_LIB", LIB_PATH)
+    if p == LIB_PATH:
+        _ensure_current(p)
     if not os.path.exists(p):
         raise NiceCoreError(
             f"libnicecore.so not found at {p}; build it with `python -m nicecore.build` "
@@ -221,11 +224,40 @@ def load(path: str | None = None):
         fn.argtypes = args
     if lib.nc_abi_version() != NC_ABI_VERSION:
         raise NiceCoreError("libnicecore.so ABI version mismatch; rebuild it")
+    want = tree_build_id()
+    got = lib.nc_build_id().decode()
+    if want is not None and got != want and os.environ.get("NICECORE_ALLOW_STALE") != "1":
+        raise NiceCoreError(f"{p} was built from other sources (nc_build_id {got}, this tree {want}); "
+                            "rebuild it with `python -m nicecore.build`")
     _lib = lib
     if os.environ.get("NICE_CORE_PROFILE") == "1":  # per-kernel timings at exit
         import atexit
         atexit.register(lib.nc_profile_report)
     return lib
+
+
+def tree_build_id() -> str | None:
+    """The source hash of the csrc/ tree next to this package (None when the sources
+    are not there, e.g. an installed copy without them)."""
+    from . import build as B
+    if not os.path.isdir(B.CSRC) or not os.path.exists(os.path.join(B.INCLUDE, "nicecore.h")):
+        return None
+    return B.source_hash()
+
+
+def _ensure_current(p: str):
+    """The in-tree library must be built from the tree's sources: a stale or missing
+    binary is rebuilt when hipcc is present (a message on stderr says so), and the
+    load below refuses it otherwise -- a forgotten rebuild cannot run old kernels."""
+    from . import build as B
+    want = tree_build_id()
+    if want is None or B.library_build_id(p) == want or os.environ.get("NICECORE_ALLOW_STALE") == "1":
+        return
+    if B.have_hipcc() and os.environ.get("NICECORE_NO_AUTOBUILD") != "1":
+        import sys
+        print(f"nicecore: {p} does not match the sources (build id {B.library_build_id(p)} vs {want}); "
+              "rebuilding", file=sys.stderr, flush=True)
+        B.build(force=True)
 
 
 def raw_stream(device) -> int:

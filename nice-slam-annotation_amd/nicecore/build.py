@@ -10,6 +10,7 @@ explicit (__builtin_fmaf, MFMA).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -28,6 +29,45 @@ SOURCES = ["nc_abi.hip", "nc_rays.hip", "nc_mlp.hip", "nc_grid.hip", "nc_det.hip
 ARCH = os.environ.get("NICECORE_ARCH", "gfx950")
 
 
+SRC_EXT = (".hip", ".h", ".hpp", ".cpp")
+BUILD_ID_TAG = b"nicecore-src-"
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) over the library's sources: every csrc/ file and
+    include/nicecore.h, by name and content.  Compiled into the library
+    (``nc_build_id()``) so that a loaded binary can be matched to the tree it sits in."""
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith(SRC_EXT))
+    for name, path in [(f, os.path.join(CSRC, f)) for f in files] + [("nicecore.h", os.path.join(INCLUDE, "nicecore.h"))]:
+        h.update(name.encode() + b"\0")
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def library_build_id(path: str = LIB) -> str | None:
+    """The source hash embedded in a built library, read from its bytes (no dlopen)."""
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    i = data.find(BUILD_ID_TAG)
+    if i < 0:
+        return None
+    return data[i + len(BUILD_ID_TAG):i + len(BUILD_ID_TAG) + 16].decode("ascii", "replace")
+
+
+def have_hipcc() -> bool:
+    try:
+        hipcc()
+        return True
+    except RuntimeError:
+        return False
+
+
 def hipcc() -> str:
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if c and os.path.exists(c):
@@ -36,11 +76,8 @@ def hipcc() -> str:
 
 
 def needs_build() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "nicecore.h")]
-    return any(os.path.getmtime(d) > t for d in deps)
+    """True unless the library exists and was built from exactly these sources."""
+    return library_build_id(LIB) != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False, extra=(), out: str | None = None) -> str:
@@ -50,7 +87,8 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str | None 
     if out is None and not force and not needs_build():
         return LIB
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
-             "-Wno-unused-function", "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC, *extra]
+             "-Wno-unused-function", "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC,
+             f'-DNC_SRC_HASH="{source_hash()}"', *extra]
     # one hipcc per source in parallel, then one link: the wall time is the slowest file
     with tempfile.TemporaryDirectory(prefix="nicecore_build_") as tmp:
         objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]

@@ -17,10 +17,29 @@ Usage (inputs live in static tensors that are refilled in place)::
 
 Constraints of capture (checked by torch): no host synchronisation inside
 ``body`` (no ``.item()``, no boolean-mask indexing) and fixed shapes.
+
+Streams (the cause of the round-4 ``capture_end`` segfault): torch
+records on every leaf's gradient accumulator (its AccumulateGrad node) the stream
+that was current when the node was created, and the autograd engine makes that
+stream wait on the producer's before it hands the leaf its gradient.  A node lives
+as long as any autograd graph that reaches it: a body that keeps its undetached
+loss (``out["loss"] = loss``) keeps every call's accumulators alive into the next
+call, so accumulators created by eager calls on the default stream are still the
+ones the captured backward reaches -- and the engine then makes the legacy default
+stream wait on an event of the capturing stream, which a capture does not allow
+(HIP crashed in ``hipStreamEndCapture``).  GraphedStep therefore warms up and
+captures on ONE stream (accumulators created by the warm-up are on the capture
+stream), and refuses, with an error naming the cause, a body whose accumulators
+belong to a graph that was alive before the GraphedStep was built.
 """
 from __future__ import annotations
 
+import gc
+import warnings
+
 import torch
+
+from ._lib import NiceCoreError
 
 
 def _detach(out):
@@ -33,20 +52,70 @@ def _detach(out):
     return out
 
 
+_WALK_LIMIT = 200_000  # autograd nodes visited per scan (a bound, not a tuning knob)
+
+
+def _live_accumulators():
+    """AccumulateGrad nodes reachable from every autograd graph alive in the process
+    (graphs are held by tensors with a grad_fn; tensors are tracked by the cyclic GC),
+    as {node: leaf tensor}."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        roots = []
+        for o in gc.get_objects():
+            try:
+                if isinstance(o, torch.Tensor) and o.grad_fn is not None:
+                    roots.append(o.grad_fn)
+            except Exception:  # objects whose isinstance / attribute access raises
+                continue
+    seen, acc, stack = set(), {}, roots
+    while stack and len(seen) < _WALK_LIMIT:
+        n = stack.pop()
+        if n is None or n in seen:
+            continue
+        seen.add(n)
+        if type(n).__name__ == "AccumulateGrad":
+            acc[n] = n.variable
+            continue
+        stack.extend(f for f, _ in n.next_functions)
+    return acc
+
+
 class GraphedStep:
     def __init__(self, body, warmup: int = 3, pool=None):
         self.body = body
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):  # warm up allocator / autograd outside capture
-            for _ in range(warmup):
-                _detach(body())
+        self.stream = side = torch.cuda.Stream()
+        # accumulators of graphs alive before the warm-up: a pre-hook on each records the
+        # stream the engine runs it on (its creation stream) if the body's backward reaches it
+        reached = []
+        handles = [n.register_prehook(lambda grads, leaf=v: reached.append((leaf, torch.cuda.current_stream())))
+                   for n, v in _live_accumulators().items() if v.is_cuda]
+        try:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm up allocator / autograd outside capture
+                for _ in range(max(1, warmup)):
+                    _detach(body())
+        finally:
+            for h in handles:
+                h.remove()
+        stale = [leaf for leaf, s in reached if s != side]
+        if stale:
+            shapes = ", ".join(sorted({str(tuple(v.shape)) for v in stale})[:4])
+            raise NiceCoreError(
+                f"GraphedStep: the body's backward reaches gradient accumulator(s) (leaf shapes {shapes}) of an "
+                "autograd graph that was alive before the GraphedStep was built -- typically a loss kept without "
+                ".detach() from an earlier eager call (e.g. out['loss'] = loss). Torch runs an accumulator on the "
+                "stream it was created on, so the captured backward would wait on that stream (the default stream "
+                "cannot join a capture). Keep loss.detach() / loss.item(), or drop the old loss, before building "
+                "the GraphedStep.")
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        # thread_local: CUDA calls of other host threads (e.g. a process group's
-        # watchdog) during the capture do not invalidate it
-        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
+        # the same stream as the warm-up: accumulators the warm-up created (and a body
+        # that keeps its own loss carries into the capture) are on the capture stream.
+        # thread_local: CUDA calls of other host threads (e.g. a process group's watchdog)
+        # during the capture do not invalidate it
+        with torch.cuda.graph(self.graph, pool=pool, stream=side, capture_error_mode="thread_local"):
             self.out = _detach(body())
 
     def __call__(self):

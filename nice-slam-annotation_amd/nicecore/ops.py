@@ -44,10 +44,11 @@ def _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_st
 
 
 def _t_rand(t_rand, perturb, n_rays, n_strat, device):
-    """The stratified samples' jitter draws (Renderer.py:211-219): the caller's, or -- when
-    perturb > 0 -- torch.rand([N, N_samples]) on the CPU's default generator moved to the
-    device, as the reference draws them; None when perturb == 0."""
-    if perturb <= 0. and t_rand is None:
+    """The stratified samples' jitter draws (Renderer.py:211-219) when perturb > 0: the
+    caller's ``t_rand``, or torch.rand([N, N_samples]) on the CPU's default generator moved
+    to the device, as the reference draws them.  None when perturb == 0 -- the reference
+    does not jitter then, so a ``t_rand`` passed with perturb == 0 is not used."""
+    if perturb <= 0.:
         return None
     if t_rand is None:
         t_rand = torch.rand(n_rays, n_strat)
@@ -64,7 +65,7 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     ``lindisp``: stratified depths linear in disparity (Renderer.py:208-209).  ``perturb``
     > 0 jitters them inside their intervals (Renderer.py:211-219) with ``t_rand``
     ([N, n_strat] uniform draws; default torch.rand on the CPU generator, as the
-    reference).
+    reference); with perturb == 0 there is no jitter and ``t_rand`` is not used.
 
     ``depth_max``: optional device scalar replacing the batch-global max(gt_depth)
     (Renderer.py:157, :194) -- pass the all-reduced max when a batch is sharded.
@@ -98,9 +99,9 @@ def render_rays(decoders, c, rays_o, rays_d, bound, stage, gt_depth=None, n_stra
     spec = {"plan": plan, "n_strat": n_strat, "n_surf": ns, "bound": bound, "depth_max": depth_max,
             "deterministic": deterministic, "sparse": sparse_grads, "lindisp": bool(lindisp), "t_rand": tr,
             "ray_valid": ray_mask}
-    if n_importance > 0:  # sample_pdf is stochastic exactly when the stratified samples are jittered
+    if n_importance > 0:  # sample_pdf(det=(perturb == 0.)), Renderer.py:247
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
-                                             depth_max, n_importance, det=(tr is None),
+                                             depth_max, n_importance, det=(perturb <= 0.),
                                              lindisp=bool(lindisp), t_rand=tr, ray_valid=ray_mask)
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c),
                               *param_inputs(spec, plan, rays_o.device, param_grads))
@@ -154,7 +155,7 @@ def render_rays_loss(decoders, c, rays_o, rays_d, bound, stage, target_depth, lo
             "defer": defer_param_grads, "lindisp": bool(lindisp), "t_rand": tr, "ray_valid": ray_mask}
     if n_importance > 0:
         spec["z_extra"] = _importance_depths(decoders, c, rays_o, rays_d, bound, stage, gt_depth, n_strat, ns,
-                                             depth_max, n_importance, det=(tr is None),
+                                             depth_max, n_importance, det=(perturb <= 0.),
                                              lindisp=bool(lindisp), t_rand=tr, ray_valid=ray_mask)
     return NiceRenderFn.apply(spec, rays_o, rays_d, gt_depth, *_grid_args(c),
                               *param_inputs(spec, plan, rays_o.device, param_grads))

@@ -145,3 +145,128 @@ def score_vs_truth(got, ref32, ref64, out_floor=2e-5, grad_floor=2e-4):
         floor = grad_floor if k.startswith("grad/") else out_floor
         res[k] = (e_hip, e_ref, max(4.0 * e_ref, floor))
     return res
+
+
+# --- per-element parity ---------------------------------------------
+# The per-tensor metric above (max error / max |ref|) cannot see a wrong value on a
+# lightly-touched voxel or a low-weight ray while it stays below 2e-4 of the tensor's
+# maximum.  The per-element gate: every element of every output and gradient must satisfy
+#     |hip - f64| <= ELEM_FACTOR * |ref32 - f64| + ELEM_ATOL_FRAC * max|f64|
+# where f64 is the oracle's float64 truth and ref32 a float32 reference on the same inputs
+# (the reference's own vectors for the golden cases, the float32 oracle otherwise): the
+# HIP path may be at most 4x as wrong as the reference's own float32 computation, element
+# by element, plus an absolute floor of 1e-6 of the tensor's largest element.
+ELEM_FACTOR = 4.0
+ELEM_ATOL_FRAC = 1e-6
+
+
+def elementwise_vs_truth(got, ref32, ref64, factor=ELEM_FACTOR, atol_frac=ELEM_ATOL_FRAC):
+    """{name: stats} over the tensors of ``ref64``: ``worst`` = max over elements of
+    |hip - f64| / (factor |ref32 - f64| + atol_frac max|f64|) (<= 1 passes), ``n_bad``
+    elements above 1, the relative L2 errors ``l2_hip`` / ``l2_ref`` = ||x - f64|| / ||f64||
+    and the per-tensor max-normalised errors ``max_hip`` / ``max_ref``."""
+    res = {}
+    for k, t64 in ref64.items():
+        if k not in got or k not in ref32:
+            res[k] = {"worst": float("inf"), "n_bad": -1, "n": 0, "missing": True}
+            continue
+        t = t64.double().reshape(-1)
+        h = got[k].double().reshape(-1)
+        r = ref32[k].double().reshape(-1)
+        scale = float(t.abs().max()) if t.numel() else 0.0
+        eh, er = (h - t).abs(), (r - t).abs()
+        allowed = factor * er + atol_frac * max(scale, 1e-300)
+        ratio = eh / allowed
+        nt = float(t.norm()) or 1e-300
+        res[k] = {"worst": float(ratio.max()) if t.numel() else 0.0, "n_bad": int((ratio > 1).sum()),
+                  "n": int(t.numel()), "l2_hip": float(eh.norm()) / nt, "l2_ref": float(er.norm()) / nt,
+                  "max_hip": float(eh.max()) / max(scale, 1e-300) if t.numel() else 0.0,
+                  "max_ref": float(er.max()) / max(scale, 1e-300) if t.numel() else 0.0}
+        if k.startswith("grad/grid_"):
+            res[k]["support"] = grid_support_diff(got[k], t64)
+    return res
+
+
+def grid_support_diff(got, ref):
+    """(voxels with a non-zero gradient only in ``got``, only in ``ref``) of [1, C, D, H, W]
+    grid gradients: a dropped or mis-addressed scatter shows here whatever its size."""
+    a = (got.reshape(got.shape[-4], -1) != 0).any(0)
+    b = (ref.reshape(ref.shape[-4], -1) != 0).any(0)
+    return int((a & ~b).sum()), int((b & ~a).sum())
+
+
+def report_elementwise(title, res):
+    """Print the per-tensor table (worst per-element ratio first) and return the failures."""
+    print(f"\n[{title}] per-element vs float64 truth (worst ratio <= 1 passes; rel-L2 hip / ref32)")
+    bad = {}
+    for k, v in sorted(res.items(), key=lambda kv: -kv[1]["worst"]):
+        sup = v.get("support")
+        print(f"  {k:44s} worst {v['worst']:.3g}  n_bad {v['n_bad']}/{v['n']}  "
+              f"l2 {v.get('l2_hip', float('nan')):.2e} / {v.get('l2_ref', float('nan')):.2e}  "
+              f"max {v.get('max_hip', float('nan')):.2e} / {v.get('max_ref', float('nan')):.2e}"
+              + (f"  support +{sup[0]} -{sup[1]}" if sup else ""))
+        if not v["worst"] <= 1.0 or (sup and sup != (0, 0)):
+            bad[k] = v
+    worst = max((v["worst"] for v in res.values()), default=0.0)
+    print(f"  worst per-element ratio over all tensors: {worst:.4g}")
+    return bad
+
+
+def collect_step(grids, model, ro, rd, outs=None, loss=None):
+    """{name: cpu tensor} of a rendered step: outputs (when given) and every non-zero
+    leaf gradient, in the oracle's naming."""
+    got = {}
+    if outs is not None:
+        d, u, c = outs
+        got.update({"depth": d.detach().cpu(), "var": u.detach().cpu(), "color": c.detach().cpu()})
+    if loss is not None:
+        got["loss"] = loss.detach().cpu().reshape(1)
+    got["grad/rays_o"], got["grad/rays_d"] = ro.grad.detach().cpu(), rd.grad.detach().cpu()
+    for k, g in grids.items():
+        if g.grad is not None and float(g.grad.abs().max()) > 0:
+            got["grad/" + k] = g.grad.detach().cpu()
+    for n, p in model.named_parameters():
+        if p.grad is not None and float(p.grad.abs().max()) > 0:
+            got["grad/param/" + n] = p.grad.detach().cpu()
+    return got
+
+
+def oracle_mapper_refs(w, kw, stage="color"):
+    """The oracle's render + Mapper loss (Mapper.py:603-612) + backward on a bench workload
+    ``w`` (bench.build_workload), in float32 and float64: {False: ref32, True: ref64}."""
+    from nicecore import scene as S
+    from oracle import nice_oracle as O
+    g_cpu = {k: v.detach().cpu().contiguous() for k, v in w["grids"].items()}
+    prm = {n: p.detach().cpu() for n, p in w["model"].named_parameters()}
+    ro, rd, gt, gtc = (t.detach().cpu() for t in (w["ro"], w["rd"], w["gt"], w["gtc"]))
+    dec_b = S.decoder_bounds(w["sc"].bound)
+    refs = {}
+    for f64 in (False, True):
+        cast = (lambda t: t.double()) if f64 else (lambda t: t)
+        ro_c, rd_c = cast(ro.clone()).requires_grad_(True), cast(rd.clone()).requires_grad_(True)
+        g_c = {k: cast(v.clone()).requires_grad_(True) for k, v in g_cpu.items()}
+        p_c = {k: cast(v.clone()).requires_grad_(True) for k, v in prm.items()}
+        with (O.float64_mode() if f64 else _null()):
+            dd, uu, cc = O.render_batch_ray(g_c, p_c, dec_b, w["sc"].bound, rd_c, ro_c, stage, cast(gt))
+            lo = O.mapper_loss(dd, cc, cast(gt), cast(gtc), kw["w_color_loss"], kw["color_term"])
+            lo.backward()
+        r = {"depth": dd.detach(), "var": uu.detach(), "color": cc.detach(), "loss": lo.detach().reshape(1),
+             "grad/rays_o": ro_c.grad, "grad/rays_d": rd_c.grad}
+        for k, t in g_c.items():
+            if t.grad is not None and float(t.grad.abs().max()) > 0:
+                r["grad/" + k] = t.grad
+        for k, t in p_c.items():
+            if t.grad is not None and float(t.grad.abs().max()) > 0:
+                r["grad/param/" + k] = t.grad
+        refs[f64] = r
+    return refs
+
+
+def c2_args(**over):
+    """bench.py's default C2 arguments (Replica room0, 1000 rays, stage color, BA)."""
+    import types
+    a = dict(scene="replica_room0", rays=1000, stage="color", mode="ba", layout="channels_last",
+             sparse_grads="auto", frustum="off", overlap="off", fix_fine=False, render_depth="target",
+             param_grads="direct", eager=True, iteration=False)
+    a.update(over)
+    return types.SimpleNamespace(**a)

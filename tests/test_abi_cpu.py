@@ -40,6 +40,30 @@ def test_library_binds_every_symbol_now():
     ctypes.CDLL(B.LIB, mode=os.RTLD_NOW | os.RTLD_LOCAL)
 
 
+def test_build_id_matches_the_tree(lib):
+    """The loaded library was compiled from these sources: its
+    nc_build_id() is the tree's source hash, also readable from the file's bytes."""
+    want = B.source_hash()
+    assert lib.nc_build_id().decode() == want
+    assert B.library_build_id(B.LIB) == want
+    assert not B.needs_build()
+    print("nc_build_id", want)
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A binary built from other sources is refused by load() (no silent old kernels)."""
+    stale = tmp_path / "libnicecore.so"
+    data = open(B.LIB, "rb").read()
+    i = data.find(B.BUILD_ID_TAG) + len(B.BUILD_ID_TAG)
+    stale.write_bytes(data[:i] + b"0123456789abcdef" + data[i + 16:])
+    assert B.library_build_id(str(stale)) == "0123456789abcdef"
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(L.NiceCoreError, match="other sources"):
+        L.load(str(stale))
+    monkeypatch.setattr(L, "_lib", None)
+    L.load()
+
+
 def test_struct_layouts_match(lib):
     assert lib.nc_struct_size(0) == ctypes.sizeof(L.NcRenderArgs)
     assert lib.nc_struct_size(1) == ctypes.sizeof(L.NcPointsArgs)

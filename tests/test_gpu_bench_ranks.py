@@ -1,7 +1,8 @@
 """bench.py's N > 1 path, run as the driver runs it (a fresh process per call), on one GPU:
-two ranks over gloo (bench.launch_ranks spawns them; RCCL needs one GPU per rank) against
-one rank, on the SAME global batch (--global-batch: rank r renders its contiguous shard of
-the 1,000 rays the single rank renders, distributed.shard).
+two or three ranks over gloo (bench.launch_ranks spawns them; RCCL needs one GPU per rank)
+against one rank, on the SAME global batch (--global-rays: rank r renders its contiguous
+shard of the rays the single rank renders, distributed.shard_bounds -- with 3 ranks the
+shards are uneven, 334 / 333 / 333), on Replica room0 and on Apartment (C4).
 
 One step after the timed ones (--dump-grads) is compared: the exchanged gradients of the
 two ranks -- the frustum rows of the three grids (the Mapper's frustum_feature_selection,
@@ -27,23 +28,31 @@ def _bench(tmp_path, name, *args):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "2",
-                        "--cpu-seconds", "0", "--global-batch", "--frustum", "on", "--dump-grads", str(out), *args],
+                        "--cpu-seconds", "0", "--frustum", "on", "--dump-grads", str(out), *args],
                        capture_output=True, text=True, timeout=400, env=env, cwd=REPO)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     return line, torch.load(out, weights_only=True)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("overlap", ["on", "off"])
-def test_two_gloo_ranks_equal_one_rank(tmp_path, overlap):
-    one_line, one = _bench(tmp_path, "one", "--gpus", "1", "--rays", "1000", "--overlap", overlap)
-    two_line, two = _bench(tmp_path, "two", "--gpus", "2", "--backend", "gloo", "--rays", "500", "--overlap", overlap)
-    assert one_line["n_gpus"] == 1 and two_line["n_gpus"] == 2
-    assert two_line["config"]["parallelism"] == "dp2" and two_line["config"]["rays_per_gpu"] == 500
-    assert two_line["config"]["grid_exchange"].startswith("frustum rows")
-    assert two_line["config"]["overlap"] == ("grid all-reduce beside k_mlp_dw" if overlap == "on" else "none")
-    assert two["world"] == 2 and one["world"] == 1
+_ONE = {}
+
+
+def _one_rank(tmp_path, scene, total):
+    """The single-rank reference of a (scene, total rays) batch, run once per module."""
+    key = (scene, total)
+    if key not in _ONE:
+        _ONE[key] = _bench(tmp_path, f"one_{scene}_{total}", "--gpus", "1", "--scene", scene,
+                           "--global-rays", str(total), "--overlap", "off")
+    return _ONE[key]
+
+
+def _check_equal(one, two, world, total):
+    from nicecore.distributed import shard_bounds
+    assert two["world"] == world and one["world"] == 1
+    assert two["total_rays"] == one["total_rays"] == total
+    a, b = shard_bounds(total, 0, world)
+    assert two["rays_per_rank"] == b - a  # rank 0's shard (the larger one when uneven)
     for k in one["frustum_rows"]:
         assert torch.equal(one["frustum_rows"][k], two["frustum_rows"][k]), k
     assert set(one["grids"]) == set(two["grids"]) and len(one["grids"]) == 3
@@ -55,3 +64,31 @@ def test_two_gloo_ranks_equal_one_rank(tmp_path, overlap):
             if not e <= 1e-5:
                 bad[f"{group}/{k}"] = e
     assert not bad, bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("overlap", ["on", "off"])
+def test_gloo_ranks_equal_one_rank(tmp_path, world, overlap):
+    """world 2 (500 + 500 rays) and world 3 (334 + 333 + 333: distributed.shard_bounds'
+    remainder) on one 1,000-ray Replica room0 batch."""
+    one_line, one = _one_rank(tmp_path, "replica_room0", 1000)
+    line, many = _bench(tmp_path, f"w{world}_{overlap}", "--gpus", str(world), "--backend", "gloo",
+                        "--global-rays", "1000", "--overlap", overlap)
+    assert one_line["n_gpus"] == 1 and line["n_gpus"] == world
+    assert line["config"]["parallelism"] == f"dp{world}"
+    assert line["config"]["grid_exchange"].startswith("frustum rows")
+    assert line["config"]["overlap"] == ("grid all-reduce beside k_mlp_dw" if overlap == "on" else "none")
+    _check_equal(one, many, world, 1000)
+
+
+@pytest.mark.gpu
+def test_gloo_ranks_apartment_frustum_rows(tmp_path):
+    """Apartment (BASELINE C4 geometry: 625 rays per GPU of a 5,000-ray window): two ranks of
+    625 rays with the frustum-row exchange against one rank of the 1,250-ray batch."""
+    one_line, one = _one_rank(tmp_path, "apartment", 1250)
+    line, two = _bench(tmp_path, "apartment_w2", "--gpus", "2", "--backend", "gloo", "--scene", "apartment",
+                       "--global-rays", "1250", "--overlap", "auto")
+    assert line["n_gpus"] == 2 and line["config"]["rays_per_gpu"] == 625
+    assert line["config"]["grid_exchange"].startswith("frustum rows")
+    _check_equal(one, two, 2, 1250)

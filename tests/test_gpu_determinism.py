@@ -154,11 +154,14 @@ def test_deterministic_graph_replay_bitwise(monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bits", ["8", "11"])
-def test_deterministic_sort_digit_width_invariant(bits, monkeypatch):
+@pytest.mark.parametrize("n_rays", [700, 2000])
+def test_deterministic_sort_digit_width_invariant(bits, n_rays, monkeypatch):
     """The radix sort's digit width (default: 2 passes of 10 bits for the room0 grids' 20-bit
     keys; NC_DET_SORT_BITS pins 8..11) changes the passes, not the result: a stable sort has
-    exactly one output, so the gradients are bit-identical to the default width's."""
-    sc, grids, params, ro, rd, dep = _room0_case(700, "color", seed=5)
+    exactly one output, so the gradients are bit-identical to the default width's.  2,000
+    rays (2.3M sort entries, more than 48 tiles per scan group) take k_rs_scan's memory
+    fallback; 700 rays its register branch."""
+    sc, grids, params, ro, rd, dep = _room0_case(n_rays, "color", seed=5)
     monkeypatch.delenv("NC_DET_SORT_BITS", raising=False)
     a = _render_grads(sc, grids, params, ro, rd, dep, "color", True)
     monkeypatch.setenv("NC_DET_SORT_BITS", bits)

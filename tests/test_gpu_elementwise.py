@@ -1,0 +1,95 @@
+"""Per-element parity against a float64 truth.
+
+Every other parity test scores a tensor by its largest error over its largest value
+(parity_common.rel_err).  That metric hides a wrong gradient on a lightly-touched voxel
+or a low-weight ray while it stays below the gate's fraction of the tensor's maximum.
+Here every element of every output and gradient is held to
+
+    |hip - f64| <= 4 |ref32 - f64| + 1e-6 max|f64|          (parity_common.ELEM_*)
+
+with f64 the oracle in float64 on the same inputs and ref32 a float32 reference: the
+reference's own vectors (tests/golden, produced by importing /root/reference) for the
+golden and init-std cases, the float32 oracle for the C2 benchmark workload.  Grid
+gradients must also have the same support: the set of voxels with a non-zero gradient
+equals the truth's (a dropped or mis-addressed scatter of any size shows there).  The
+C2 workload is scored both eager and as the graph-replayed step bench.py times
+(bench.make_step(...)[1]).  Each test prints the per-tensor table: worst per-element
+ratio, relative L2 error of HIP and of ref32, and the max-normalised errors.
+
+Reference: src/utils/Renderer.py:95-262 (render_batch_ray), src/conv_onet/models/
+decoder.py:179-219 (grid_sample + MLP; the grid_sampler_3d backward scatter at :186),
+src/Mapper.py:603-612 (the Mapper loss)."""
+import pytest
+import torch
+
+from conftest import CASE_NAMES, INITSTD_CASES, load_case
+from parity_common import (c2_args, case_stage, collect_step, oracle_mapper_refs, oracle_render_grads,
+                           report_elementwise, elementwise_vs_truth, run_case, scene_of)
+from conftest import load_scene
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASE_NAMES + INITSTD_CASES)
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_golden_elementwise(case, channels_last):
+    rec, got = run_case(case, channels_last=channels_last)
+    bound, cbound, grids, params = load_scene(scene_of(case))
+    stage, with_depth = case_stage(case)
+    dec_b = {"coarse": cbound, "middle": bound, "fine": bound, "color": bound}
+    gt = rec["gt_depth"] if with_depth else None
+    ref64 = oracle_render_grads(grids, params, dec_b, bound, rec["rays_o"], rec["rays_d"], stage, gt,
+                                (rec["g_depth"], rec["g_var"], rec["g_color"]), f64=True)
+    ref64 = {k: v for k, v in ref64.items() if k in rec}  # the tensors the reference produced
+    res = elementwise_vs_truth(got, rec, ref64)
+    bad = report_elementwise(f"{case} {'channels_last' if channels_last else 'ncdhw'}", res)
+    assert not bad, bad
+
+
+def _c2_eager_and_graphed():
+    import bench
+    dev = torch.device("cuda", 0)
+    args = c2_args(eager=False)
+    w = bench.build_workload(args, 0, dev)
+    eager, graphed = bench.make_step(w, args, 1, dev)
+    out = {}
+    for _ in range(3):  # several replays: each rewrites every gradient from zero
+        graphed()
+    torch.cuda.synchronize()
+    out["graphed"] = collect_step(w["grids"], w["model"], w["ro"], w["rd"], None, graphed.step.out)
+    # eager, with the outputs: the call the captured body makes (bench.make_step.body)
+    grids, model = w["grids"], w["model"]
+    for t in list(grids.values()) + list(model.parameters()) + [w["ro"], w["rd"]]:
+        t.grad = None
+    d, u, c, loss = w["renderer"].render_batch_loss(grids, model, w["rd"], w["ro"], dev, "color", w["gt"],
+                                                    w["gtc"], **bench.LOSS_KW["ba"]("color"),
+                                                    render_gt_depth="target")
+    loss.backward()
+    torch.cuda.synchronize()
+    out["eager"] = collect_step(grids, model, w["ro"], w["rd"], (d, u, c), loss)
+    return w, out
+
+
+@pytest.mark.gpu
+def test_c2_workload_elementwise_eager_and_graphed():
+    """bench.py's C2 workload (room0, 1000 rays x 48 samples, the reference's grid_init
+    statistics, channels-last grids, the fused Mapper loss, BA gradients): the eager step and
+    the graph-replayed step the bench times, each against the oracle's float32 / float64
+    render + loss + backward, per element; and the two HIP forms against each other."""
+    import bench
+    w, out = _c2_eager_and_graphed()
+    refs = oracle_mapper_refs(w, bench.LOSS_KW["ba"]("color"))
+    bad = {}
+    for form in ("eager", "graphed"):
+        truth = refs[True] if form == "eager" else {k: v for k, v in refs[True].items()
+                                                    if k not in ("depth", "var", "color")}
+        res = elementwise_vs_truth(out[form], refs[False], truth)
+        bad.update({f"{form}:{k}": v for k, v in report_elementwise(f"C2 {form}", res).items()})
+    # the replayed step against the eager one: ray and parameter gradients bit-identical
+    # (fixed-order reductions), grid gradients to float-atomic order
+    for k, g in out["graphed"].items():
+        v = out["eager"][k]
+        if k.startswith("grad/grid_"):
+            assert float((g - v).abs().max()) <= 1e-6 * float(v.abs().max()), k
+        else:
+            assert torch.equal(g, v), k
+    assert not bad, bad

@@ -88,8 +88,13 @@ def _run(sc, grids, params, ro, rd, dep, col, mask, mode, fused):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,fused", [("ba", True), ("ba", False), ("tracker", True)])
-def test_masked_equals_compacted(mode, fused):
-    sc, grids, params, ro, rd, dep, col, keep = _case(600)
+@pytest.mark.parametrize("n_rays", [600, 5000])
+def test_masked_equals_compacted(mode, fused, n_rays):
+    """5,000 rays (ScanNet tracking's pixel count, the Mapper's BA batch size) take the
+    masked paths that only run above 4,096 rays -- k_depth_max's kept-ray filter and k_loss's
+    uncached median over the kept rays -- while the ~3,750-ray compacted batch takes the
+    cached ones."""
+    sc, grids, params, ro, rd, dep, col, keep = _case(n_rays)
     assert DROP_FRAC * 0.8 < float((~keep).float().mean()) < DROP_FRAC * 1.2
     om, lm, gm = _run(sc, grids, params, ro, rd, dep, col, keep, mode, fused)
     oc, lc, gc = _run(sc, grids, params, ro[keep], rd[keep], dep[keep], col[keep], None, mode, fused)

@@ -107,3 +107,18 @@ def test_render_template_fields():
     assert t.bound[0][1] == float(b[0, 1])
     assert t.dec[L.DEC_COLOR].out_w == m.color_decoder.output_linear.weight.data_ptr()
     assert plan.render_template(torch.device("cpu"), 32, 16, b) is t
+
+
+def test_graph_live_accumulator_scan():
+    """nicecore.graph._live_accumulators finds the gradient accumulators of an autograd
+    graph held only by a container (the round-4 capture_end crash pattern),
+    and forgets them once the graph is dropped."""
+    import torch
+    from nicecore.graph import _live_accumulators
+    a = torch.zeros(3, requires_grad=True)
+    b = torch.ones(2, requires_grad=True)
+    held = {"loss": (a * 2).sum() + (b * b).sum()}
+    leaves = list(_live_accumulators().values())
+    assert any(v is a for v in leaves) and any(v is b for v in leaves)
+    held.clear()
+    assert not any(v is a or v is b for v in _live_accumulators().values())

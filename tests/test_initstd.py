@@ -14,8 +14,6 @@ the split-f16 forward GEMM works in.
     1000 rays x 48 samples, the bench's seeds and init) scored against a float64 oracle
     truth beside the fp32 oracle (parity_common.score_vs_truth).
 """
-import types
-
 import pytest
 import torch
 
@@ -92,51 +90,16 @@ def test_bench_c2_workload_against_oracle():
     float64.  Outputs and every gradient must stay within max(4x the fp32 oracle's own
     error vs float64, floor)."""
     import bench
-    from parity_common import score_vs_truth
-    from nicecore import scene as S
-    args = types.SimpleNamespace(scene="replica_room0", rays=1000, stage="color", mode="ba", layout="channels_last",
-                                 sparse_grads="auto", frustum="off", overlap="off", fix_fine=False,
-                                 render_depth="target", param_grads="direct", eager=True, iteration=False)
+    from parity_common import c2_args, collect_step, oracle_mapper_refs, score_vs_truth
     dev = torch.device("cuda", 0)
-    w = bench.build_workload(args, 0, dev)
+    w = bench.build_workload(c2_args(), 0, dev)
     grids, model, renderer = w["grids"], w["model"], w["renderer"]
     kw = bench.LOSS_KW["ba"]("color")
     d, u, c, loss = renderer.render_batch_loss(grids, model, w["rd"], w["ro"], dev, "color", w["gt"], w["gtc"],
                                                **kw, render_gt_depth="target")
     loss.backward()
-    got = {"depth": d.detach().cpu(), "var": u.detach().cpu(), "color": c.detach().cpu(),
-           "loss": loss.detach().cpu().reshape(1),
-           "grad/rays_o": w["ro"].grad.cpu(), "grad/rays_d": w["rd"].grad.cpu()}
-    for k, g in grids.items():
-        if g.grad is not None and float(g.grad.abs().max()) > 0:
-            got["grad/" + k] = g.grad.cpu()
-    for n, p in model.named_parameters():
-        if p.grad is not None and float(p.grad.abs().max()) > 0:
-            got["grad/param/" + n] = p.grad.cpu()
-    # the oracle on the identical inputs
-    g_cpu = {k: v.detach().cpu().contiguous() for k, v in grids.items()}
-    prm = {n: p.detach().cpu() for n, p in model.named_parameters()}
-    ro, rd, gt, gtc = (t.detach().cpu() for t in (w["ro"], w["rd"], w["gt"], w["gtc"]))
-    dec_b = S.decoder_bounds(w["sc"].bound)
-    refs = {}
-    for f64 in (False, True):
-        cast = (lambda t: t.double()) if f64 else (lambda t: t)
-        ro_c, rd_c = cast(ro.clone()).requires_grad_(True), cast(rd.clone()).requires_grad_(True)
-        g_c = {k: cast(v.clone()).requires_grad_(True) for k, v in g_cpu.items()}
-        p_c = {k: cast(v.clone()).requires_grad_(True) for k, v in prm.items()}
-        with (O.float64_mode() if f64 else _null()):
-            dd, uu, cc = O.render_batch_ray(g_c, p_c, dec_b, w["sc"].bound, rd_c, ro_c, "color", cast(gt))
-            lo = O.mapper_loss(dd, cc, cast(gt), cast(gtc), kw["w_color_loss"], kw["color_term"])
-            lo.backward()
-        r = {"depth": dd.detach(), "var": uu.detach(), "color": cc.detach(), "loss": lo.detach().reshape(1),
-             "grad/rays_o": ro_c.grad, "grad/rays_d": rd_c.grad}
-        for k, t in g_c.items():
-            if t.grad is not None and float(t.grad.abs().max()) > 0:
-                r["grad/" + k] = t.grad
-        for k, t in p_c.items():
-            if t.grad is not None and float(t.grad.abs().max()) > 0:
-                r["grad/param/" + k] = t.grad
-        refs[f64] = r
+    got = collect_step(grids, model, w["ro"], w["rd"], (d, u, c), loss)
+    refs = oracle_mapper_refs(w, kw)
     scores = score_vs_truth(got, refs[False], refs[True])
     bad = {k: v for k, v in scores.items() if not v[0] <= v[2]}
     assert not bad, bad
