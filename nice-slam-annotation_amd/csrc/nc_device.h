@@ -167,6 +167,16 @@ __host__ __device__ constexpr int hslot(int f) { return 8 * ((f >> 2) & 3) + 4 *
 
 // split 8 C-layout values (one 32-feature block of a lane) into f16 hi / scaled lo
 __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
+#ifdef NC_ABL_NO_SPLIT  // timing-only ablation: hi only, no lo half (results wrong)
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const halfx2 h = __builtin_amdgcn_cvt_pkrtz(x[j], x[j + 1]);
+    hi[j] = (_Float16)h[0];
+    hi[j + 1] = (_Float16)h[1];
+    lo[j] = lo[j + 1] = (_Float16)0.f;
+  }
+  return;
+#endif
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
     const halfx2 h = __builtin_amdgcn_cvt_pkrtz(x[j], x[j + 1]);
@@ -344,7 +354,11 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
   for (int k = 0; k < 8; ++k) {
     const bool in = VEC || ((c.inb >> k) & 1u);
 #pragma unroll
+#ifdef NC_ABL_NO_TRIW  // timing-only ablation: no weight products (results wrong)
+    for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[k][j] : 0.f);
+#else
     for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[k][j] * c.w[k] : 0.f);
+#endif
   }
 }
 
@@ -376,7 +390,11 @@ __device__ __forceinline__ void gather8x2(const nc_grid& G1, const Corners& c1, 
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
 #pragma unroll
+#ifdef NC_ABL_NO_TRIW  // timing-only ablation: no weight products (results wrong)
+      for (int j = 0; j < 8; ++j) out[j] = out[j] + v[q][k][j];
+#else
       for (int j = 0; j < 8; ++j) out[j] = out[j] + v[q][k][j] * c.w[k];  // 0 * w from the zero row
+#endif
     }
   }
 }

@@ -25,16 +25,28 @@ import torch.nn.functional as F
 # (FLOAT = torch.float32); tests switch it to float64 with ``float64_mode()`` to
 # obtain a ground truth against which both fp32 implementations are scored.
 FLOAT = torch.float32
+# float64 mode with the reference's explicit input roundings kept: the lookup coordinates
+# (decoder.py:182 ``vgrid = p_nor[:, :, None, None].float()``) and the Fourier input
+# (``p.float()``) rounded to float32 first, everything after them in float64 -- the exact-
+# arithmetic value of the reference's float32 program, the per-element truth of
+# tests/test_gpu_elementwise.py.  Plain float64_mode() computes from the unrounded points.
+ROUND32 = False
 
 
 @contextlib.contextmanager
-def float64_mode():
-    global FLOAT
-    old, FLOAT = FLOAT, torch.float64
+def float64_mode(round_inputs: bool = False):
+    global FLOAT, ROUND32
+    old, oldr = FLOAT, ROUND32
+    FLOAT, ROUND32 = torch.float64, round_inputs
     try:
         yield
     finally:
-        FLOAT = old
+        FLOAT, ROUND32 = old, oldr
+
+
+def _in32(t: torch.Tensor) -> torch.Tensor:
+    """An input the reference rounds to float32, in the compute dtype."""
+    return t.to(torch.float32).to(FLOAT) if ROUND32 else t.to(FLOAT)
 
 STAGE_DECODERS = {  # decoder.py:341-370 (which MLPs feed raw at each stage)
     "coarse": ("coarse",),
@@ -78,7 +90,7 @@ def sample_grid_window(p, window, bound, full_dims, offset):
     order.  The window offset is subtracted from the integer corner indices only, so the
     weights are those of the full grid, bit for bit.  A corner outside the window that is
     inside the full grid raises (the caller sized the window too small).  Returns [P, C]."""
-    vn = normalize_3d_coordinate(p, bound).to(FLOAT)
+    vn = _in32(normalize_3d_coordinate(p, bound))
     D, H, W = full_dims
     z0, y0, x0 = offset
     d, h, w = window.shape[2:]
@@ -118,7 +130,7 @@ def sample_grid_feature(p: torch.Tensor, grid: torch.Tensor, bound: torch.Tensor
     align_corners=True.  Returns [P, C]."""
     if key in _WINDOWS:
         return sample_grid_window(p, grid, bound, *_WINDOWS[key])
-    vgrid = normalize_3d_coordinate(p, bound).unsqueeze(0)[:, :, None, None].to(FLOAT)
+    vgrid = _in32(normalize_3d_coordinate(p, bound).unsqueeze(0)[:, :, None, None])
     c = F.grid_sample(grid, vgrid, padding_mode='border', align_corners=True, mode='bilinear')
     return c.squeeze(-1).squeeze(-1).transpose(1, 2).squeeze(0)
 
@@ -134,7 +146,7 @@ def mlp_forward(p, grids, prm, pre, name, bound, color=False, concat=False):
         with torch.no_grad():
             c_mid = sample_grid_feature(p, grids['grid_middle'], bound, 'grid_middle')
         c = torch.cat([c, c_mid], dim=1)
-    pf = p.to(FLOAT)
+    pf = _in32(p)
     emb = torch.sin(pf @ prm[pre + 'embedder._B'])  # decoder.py:26-30
     h = emb
     for i in range(5):

@@ -97,18 +97,30 @@ def compare(rec, got):
     return out
 
 
-def oracle_render_grads(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, f64=False, depth_max=None):
+def oracle_render_grads(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, f64=False, depth_max=None,
+                        round_inputs=False, order=None):
     """CPU oracle render + backward; with f64=True everything runs in float64
-    (ground truth).  ``depth_max``: the batch-global max(gt_depth) of a sharded batch.
-    Returns {name: tensor} like run_case."""
+    (ground truth; ``round_inputs``: keeping the reference's float32 input roundings,
+    nice_oracle.float64_mode).  ``depth_max``: the batch-global max(gt_depth) of a sharded
+    batch.  ``order``: a permutation the rays are rendered in (results un-permuted): the
+    same float32 program with other summation orders.  Returns {name: tensor} like run_case."""
     from oracle import nice_oracle as O
+    if order is not None:
+        inv = torch.argsort(order)
+        gd, gv, gc = upstream
+        out = oracle_render_grads(grids, params, dec_b, bound, ro[order], rd[order], stage,
+                                  gt[order] if gt is not None else None, (gd[order], gv[order], gc[order]),
+                                  f64, depth_max, round_inputs)
+        for k in ("depth", "var", "color", "grad/rays_o", "grad/rays_d"):
+            out[k] = out[k][inv]
+        return out
     cast = (lambda t: t.double()) if f64 else (lambda t: t)
     ro_c = cast(ro.clone()).requires_grad_(True)
     rd_c = cast(rd.clone()).requires_grad_(True)
     g_c = {k: cast(v.clone()).requires_grad_(True) for k, v in grids.items()}
     prm_c = {k: cast(v.clone()).requires_grad_(True) for k, v in params.items()}
     gt_c = cast(gt) if gt is not None else None
-    ctx = O.float64_mode() if f64 else _null()
+    ctx = O.float64_mode(round_inputs) if f64 else _null()
     with ctx:
         dm = None if depth_max is None else cast(depth_max.reshape(()).clone())
         d, v, c = O.render_batch_ray(g_c, prm_c, dec_b, bound, rd_c, ro_c, stage, gt_c, depth_max=dm)
@@ -150,46 +162,59 @@ def score_vs_truth(got, ref32, ref64, out_floor=2e-5, grad_floor=2e-4):
 # --- per-element parity ---------------------------------------------
 # The per-tensor metric above (max error / max |ref|) cannot see a wrong value on a
 # lightly-touched voxel or a low-weight ray while it stays below 2e-4 of the tensor's
-# maximum.  The per-element gate: every element of every output and gradient must satisfy
-#     |hip - f64| <= ELEM_FACTOR * |ref32 - f64| + ELEM_ATOL_FRAC * max|f64|
-# where f64 is the oracle's float64 truth and ref32 a float32 reference on the same inputs
-# (the reference's own vectors for the golden cases, the float32 oracle otherwise): the
-# HIP path may be at most 4x as wrong as the reference's own float32 computation, element
-# by element, plus an absolute floor of 1e-6 of the tensor's largest element.
+# maximum.  The per-element gate, for every element e of every output and gradient:
+#     |hip_e - t_e| <= ELEM_FACTOR * max_k |ref_k,e - t_e| + ELEM_FACTOR * rms_e(ref_0 - t)
+# t: the oracle in float64 with the reference's float32 input roundings (p.float(), the
+#    float32 lookup coordinates: nice_oracle.float64_mode(round_inputs=True)), i.e. the exact
+#    value of the reference's float32 program;
+# ref_k: float32 computations of the same program -- ref_0 the reference's own vectors
+#    (golden cases) or the float32 oracle, ref_1.. the float32 oracle with the rays in another
+#    order (other summation orders of every reduction over points);
+# the floor: 4x the reference's own RMS float32 error over the tensor -- below 1e-6 of the
+#    tensor's max for the large tensors, above it where float32 itself is that far off (the
+#    reference's own max error reaches 5.6e-6 of max on the golden decoder gradients).
+# Grid gradients must also have the support of ref_0: the same voxels non-zero.
 ELEM_FACTOR = 4.0
-ELEM_ATOL_FRAC = 1e-6
 
 
-def elementwise_vs_truth(got, ref32, ref64, factor=ELEM_FACTOR, atol_frac=ELEM_ATOL_FRAC):
-    """{name: stats} over the tensors of ``ref64``: ``worst`` = max over elements of
-    |hip - f64| / (factor |ref32 - f64| + atol_frac max|f64|) (<= 1 passes), ``n_bad``
-    elements above 1, the relative L2 errors ``l2_hip`` / ``l2_ref`` = ||x - f64|| / ||f64||
-    and the per-tensor max-normalised errors ``max_hip`` / ``max_ref``."""
+def elementwise_vs_truth(got, refs, truth, factor=ELEM_FACTOR):
+    """{name: stats} over the tensors of ``truth``; ``refs``: one float32 reference dict or a
+    list of them (the first one sets the floor and the support).  ``worst`` = max over
+    elements of |hip - t| / allowed (<= 1 passes), ``n_bad`` elements above 1, relative L2
+    errors ``l2_hip`` / ``l2_ref`` = ||x - t|| / ||t||, max-normalised errors ``max_hip`` /
+    ``max_ref`` and the floor in units of the tensor's max, ``floor``."""
+    refs = refs if isinstance(refs, (list, tuple)) else [refs]
     res = {}
-    for k, t64 in ref64.items():
-        if k not in got or k not in ref32:
+    for k, t64 in truth.items():
+        if k not in got or any(k not in r for r in refs):
             res[k] = {"worst": float("inf"), "n_bad": -1, "n": 0, "missing": True}
             continue
         t = t64.double().reshape(-1)
+        if not t.numel():
+            res[k] = {"worst": 0.0, "n_bad": 0, "n": 0}
+            continue
         h = got[k].double().reshape(-1)
-        r = ref32[k].double().reshape(-1)
-        scale = float(t.abs().max()) if t.numel() else 0.0
-        eh, er = (h - t).abs(), (r - t).abs()
-        allowed = factor * er + atol_frac * max(scale, 1e-300)
-        ratio = eh / allowed
+        ers = [(r[k].double().reshape(-1) - t).abs() for r in refs]
+        er = torch.stack(ers).amax(0)
+        scale = max(float(t.abs().max()), 1e-300)
+        floor = factor * float(ers[0].pow(2).mean().sqrt())
+        eh = (h - t).abs()
+        ratio = eh / (factor * er + max(floor, 1e-300))
         nt = float(t.norm()) or 1e-300
-        res[k] = {"worst": float(ratio.max()) if t.numel() else 0.0, "n_bad": int((ratio > 1).sum()),
-                  "n": int(t.numel()), "l2_hip": float(eh.norm()) / nt, "l2_ref": float(er.norm()) / nt,
-                  "max_hip": float(eh.max()) / max(scale, 1e-300) if t.numel() else 0.0,
-                  "max_ref": float(er.max()) / max(scale, 1e-300) if t.numel() else 0.0}
+        res[k] = {"worst": float(ratio.max()), "n_bad": int((ratio > 1).sum()), "n": int(t.numel()),
+                  "l2_hip": float(eh.norm()) / nt, "l2_ref": float(ers[0].norm()) / nt,
+                  "max_hip": float(eh.max()) / scale, "max_ref": float(ers[0].max()) / scale,
+                  "floor": floor / scale}
         if k.startswith("grad/grid_"):
-            res[k]["support"] = grid_support_diff(got[k], t64)
+            res[k]["support"] = grid_support_diff(got[k], refs[0][k])
     return res
 
 
 def grid_support_diff(got, ref):
     """(voxels with a non-zero gradient only in ``got``, only in ``ref``) of [1, C, D, H, W]
-    grid gradients: a dropped or mis-addressed scatter shows here whatever its size."""
+    grid gradients: a dropped or mis-addressed scatter shows here whatever its size.  ``ref``
+    must make the same float32 corner decisions (the float32 reference, not a float64 truth:
+    a coordinate within an ulp of a voxel plane picks other corners in float64)."""
     a = (got.reshape(got.shape[-4], -1) != 0).any(0)
     b = (ref.reshape(ref.shape[-4], -1) != 0).any(0)
     return int((a & ~b).sum()), int((b & ~a).sum())
@@ -197,13 +222,15 @@ def grid_support_diff(got, ref):
 
 def report_elementwise(title, res):
     """Print the per-tensor table (worst per-element ratio first) and return the failures."""
-    print(f"\n[{title}] per-element vs float64 truth (worst ratio <= 1 passes; rel-L2 hip / ref32)")
+    print(f"\n[{title}] per-element vs float64 truth (worst ratio <= 1 passes; rel-L2 and max-normalised "
+          f"errors hip / ref32; floor in units of max)")
     bad = {}
     for k, v in sorted(res.items(), key=lambda kv: -kv[1]["worst"]):
         sup = v.get("support")
         print(f"  {k:44s} worst {v['worst']:.3g}  n_bad {v['n_bad']}/{v['n']}  "
               f"l2 {v.get('l2_hip', float('nan')):.2e} / {v.get('l2_ref', float('nan')):.2e}  "
-              f"max {v.get('max_hip', float('nan')):.2e} / {v.get('max_ref', float('nan')):.2e}"
+              f"max {v.get('max_hip', float('nan')):.2e} / {v.get('max_ref', float('nan')):.2e}  "
+              f"floor {v.get('floor', float('nan')):.1e}"
               + (f"  support +{sup[0]} -{sup[1]}" if sup else ""))
         if not v["worst"] <= 1.0 or (sup and sup != (0, 0)):
             bad[k] = v
@@ -231,34 +258,48 @@ def collect_step(grids, model, ro, rd, outs=None, loss=None):
     return got
 
 
-def oracle_mapper_refs(w, kw, stage="color"):
+def oracle_mapper_refs(w, kw, stage="color", forms=((False, False, None), (True, False, None))):
     """The oracle's render + Mapper loss (Mapper.py:603-612) + backward on a bench workload
-    ``w`` (bench.build_workload), in float32 and float64: {False: ref32, True: ref64}."""
+    ``w`` (bench.build_workload).  ``forms``: (float64, round_inputs, order) per result --
+    float32 / float64 computations, the float64 one with the reference's float32 input
+    roundings, or the rays in another order (outputs and ray gradients un-permuted).
+    Returns {form: {name: tensor}}; the default forms give {(False, False, None): ref32,
+    (True, False, None): ref64}, also reachable as [False] / [True]."""
     from nicecore import scene as S
     from oracle import nice_oracle as O
     g_cpu = {k: v.detach().cpu().contiguous() for k, v in w["grids"].items()}
     prm = {n: p.detach().cpu() for n, p in w["model"].named_parameters()}
-    ro, rd, gt, gtc = (t.detach().cpu() for t in (w["ro"], w["rd"], w["gt"], w["gtc"]))
+    ro0, rd0, gt0, gtc0 = (t.detach().cpu() for t in (w["ro"], w["rd"], w["gt"], w["gtc"]))
     dec_b = S.decoder_bounds(w["sc"].bound)
     refs = {}
-    for f64 in (False, True):
+    for form in forms:
+        f64, rnd, order = form
+        ro, rd, gt, gtc = (t if order is None else t[order] for t in (ro0, rd0, gt0, gtc0))
         cast = (lambda t: t.double()) if f64 else (lambda t: t)
         ro_c, rd_c = cast(ro.clone()).requires_grad_(True), cast(rd.clone()).requires_grad_(True)
         g_c = {k: cast(v.clone()).requires_grad_(True) for k, v in g_cpu.items()}
         p_c = {k: cast(v.clone()).requires_grad_(True) for k, v in prm.items()}
-        with (O.float64_mode() if f64 else _null()):
+        with (O.float64_mode(rnd) if f64 else _null()):
             dd, uu, cc = O.render_batch_ray(g_c, p_c, dec_b, w["sc"].bound, rd_c, ro_c, stage, cast(gt))
             lo = O.mapper_loss(dd, cc, cast(gt), cast(gtc), kw["w_color_loss"], kw["color_term"])
             lo.backward()
         r = {"depth": dd.detach(), "var": uu.detach(), "color": cc.detach(), "loss": lo.detach().reshape(1),
              "grad/rays_o": ro_c.grad, "grad/rays_d": rd_c.grad}
+        if order is not None:
+            inv = torch.argsort(order)
+            for k in ("depth", "var", "color", "grad/rays_o", "grad/rays_d"):
+                r[k] = r[k][inv]
         for k, t in g_c.items():
             if t.grad is not None and float(t.grad.abs().max()) > 0:
                 r["grad/" + k] = t.grad
         for k, t in p_c.items():
             if t.grad is not None and float(t.grad.abs().max()) > 0:
                 r["grad/param/" + k] = t.grad
-        refs[f64] = r
+        refs[form] = r
+    if (False, False, None) in refs:
+        refs[False] = refs[(False, False, None)]
+    if (True, False, None) in refs:
+        refs[True] = refs[(True, False, None)]
     return refs
 
 

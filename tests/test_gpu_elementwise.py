@@ -3,18 +3,28 @@
 Every other parity test scores a tensor by its largest error over its largest value
 (parity_common.rel_err).  That metric hides a wrong gradient on a lightly-touched voxel
 or a low-weight ray while it stays below the gate's fraction of the tensor's maximum.
-Here every element of every output and gradient is held to
+Here every element of every output and gradient is held to (parity_common.ELEM_FACTOR)
 
-    |hip - f64| <= 4 |ref32 - f64| + 1e-6 max|f64|          (parity_common.ELEM_*)
+    |hip - t| <= 4 max_k |ref_k - t| + 4 rms(ref_0 - t)
 
-with f64 the oracle in float64 on the same inputs and ref32 a float32 reference: the
-reference's own vectors (tests/golden, produced by importing /root/reference) for the
-golden and init-std cases, the float32 oracle for the C2 benchmark workload.  Grid
-gradients must also have the same support: the set of voxels with a non-zero gradient
-equals the truth's (a dropped or mis-addressed scatter of any size shows there).  The
-C2 workload is scored both eager and as the graph-replayed step bench.py times
-(bench.make_step(...)[1]).  Each test prints the per-tensor table: worst per-element
-ratio, relative L2 error of HIP and of ref32, and the max-normalised errors.
+t: the oracle in float64 keeping the reference's float32 input roundings (p.float(), the
+float32 lookup coordinates) -- the exact value of the reference's float32 program;
+ref_0: the reference's own vectors (tests/golden, produced by importing /root/reference)
+for the golden and init-std cases, the float32 oracle for the C2 benchmark workload;
+ref_1: the float32 oracle with the rays in reverse order (every reduction over points in
+another order).  The floor, 4x the reference's own RMS error over the tensor, is far
+below the tensor's max (a voxel's wrong gradient shows unless it is within float32 noise).
+Grid gradients must also have ref_0's support: the same voxels with a non-zero gradient
+(a dropped or mis-addressed scatter of any size shows there).  The C2 workload is scored
+both eager and as the graph-replayed step bench.py times (bench.make_step(...)[1]).
+Each test prints the per-tensor table: worst per-element ratio, relative L2 and
+max-normalised errors of HIP and of ref_0, and the floor.
+
+Why not a fixed atol of 1e-6 of the max (VERDICT r04's suggestion): the reference's own
+float32 error is above it -- up to 5.6e-6 of the max on the golden decoder gradients
+(profiles/r05/elementwise/), so an independent float32 implementation cannot meet it; and
+with a single float32 reference, an element where it happens to land on the truth
+leaves no room for any other summation order.
 
 Reference: src/utils/Renderer.py:95-262 (render_batch_ray), src/conv_onet/models/
 decoder.py:179-219 (grid_sample + MLP; the grid_sampler_3d backward scatter at :186),
@@ -37,10 +47,12 @@ def test_golden_elementwise(case, channels_last):
     stage, with_depth = case_stage(case)
     dec_b = {"coarse": cbound, "middle": bound, "fine": bound, "color": bound}
     gt = rec["gt_depth"] if with_depth else None
-    ref64 = oracle_render_grads(grids, params, dec_b, bound, rec["rays_o"], rec["rays_d"], stage, gt,
-                                (rec["g_depth"], rec["g_var"], rec["g_color"]), f64=True)
-    ref64 = {k: v for k, v in ref64.items() if k in rec}  # the tensors the reference produced
-    res = elementwise_vs_truth(got, rec, ref64)
+    args = (grids, params, dec_b, bound, rec["rays_o"], rec["rays_d"], stage, gt,
+            (rec["g_depth"], rec["g_var"], rec["g_color"]))
+    truth = oracle_render_grads(*args, f64=True, round_inputs=True)
+    truth = {k: v for k, v in truth.items() if k in rec}  # the tensors the reference produced
+    rev = oracle_render_grads(*args, order=torch.arange(rec["rays_o"].shape[0] - 1, -1, -1))
+    res = elementwise_vs_truth(got, [rec, rev], truth)
     bad = report_elementwise(f"{case} {'channels_last' if channels_last else 'ncdhw'}", res)
     assert not bad, bad
 
@@ -77,12 +89,14 @@ def test_c2_workload_elementwise_eager_and_graphed():
     render + loss + backward, per element; and the two HIP forms against each other."""
     import bench
     w, out = _c2_eager_and_graphed()
-    refs = oracle_mapper_refs(w, bench.LOSS_KW["ba"]("color"))
+    rev = torch.arange(w["ro"].shape[0] - 1, -1, -1)
+    f32, f32r, t64 = (False, False, None), (False, False, rev), (True, True, None)
+    refs = oracle_mapper_refs(w, bench.LOSS_KW["ba"]("color"), forms=(f32, f32r, t64))
     bad = {}
     for form in ("eager", "graphed"):
-        truth = refs[True] if form == "eager" else {k: v for k, v in refs[True].items()
-                                                    if k not in ("depth", "var", "color")}
-        res = elementwise_vs_truth(out[form], refs[False], truth)
+        truth = refs[t64] if form == "eager" else {k: v for k, v in refs[t64].items()
+                                                   if k not in ("depth", "var", "color")}
+        res = elementwise_vs_truth(out[form], [refs[f32], refs[f32r]], truth)
         bad.update({f"{form}:{k}": v for k, v in report_elementwise(f"C2 {form}", res).items()})
     # the replayed step against the eager one: ray and parameter gradients bit-identical
     # (fixed-order reductions), grid gradients to float-atomic order

@@ -77,6 +77,8 @@ VARIANTS = {
     "rs_r32": ["-DNC_RS_ROUNDS=32"],
     "det_rg4": ["-DNC_DET_RG=4"],  # NC_DETERMINISTIC=1 runs
     "det_rg16": ["-DNC_DET_RG=16"],
+    "no_split": ["-DNC_ABL_NO_SPLIT"],
+    "no_triw": ["-DNC_ABL_NO_TRIW"],
     "pr8": ["-DNC_PR_AHEAD=8"],
     "pr12": ["-DNC_PR_AHEAD=12"],
     "scan_d8": ["-DNC_RS_SCAN_DIG=8"],
