@@ -367,6 +367,11 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
 // lookup is accumulated exactly as gather8 (bit-identical).
 __device__ __forceinline__ void gather8x2(const nc_grid& G1, const Corners& c1, const nc_grid& G2, const Corners& c2,
                                           int g, float out1[8], float out2[8]) {
+#ifdef NC_ABL_NO_GATHER  // timing-only ablation: no global loads
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { out1[j] = c1.w[j] * 0.01f; out2[j] = c2.w[j] * 0.01f; }
+  return;
+#endif
   float v[2][8][8];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {

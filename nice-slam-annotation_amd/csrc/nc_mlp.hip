@@ -1242,9 +1242,13 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
     yrow[s] = g * LY::RS + yoff;
     xrow[s] = g * LY::RS + xoff;
   }
-  float bsum[NS];  // per-lane partial bias sums (rows 16*to+i), reduced once at the end
+  // per-lane partial bias sums (rows 16*to+i), reduced once at the end: in float64, as a
+  // bias gradient is a sum over every point of the workgroup with heavy cancellation
+  // (sum_p d out_p of an occupancy decoder), where a float32 running sum over ~10^3 points
+  // was 70x less accurate than the reference's pairwise sum (tests/test_gpu_elementwise.py)
+  double bsum[NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) bsum[s] = 0.f;
+  for (int s = 0; s < NS; ++s) bsum[s] = 0.0;
   // ---- staging: the records of the next sub-chunk are prefetched into registers
   // (branch-free, PER float4 per thread) while the current one is consumed ----
   // A sub-chunk's records are one contiguous block of DW_NPTS * STRIDE floats: item k
@@ -1328,7 +1332,7 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
         for (int s = 0; s < NC; ++s) {
           const float av = buf[yrow[s] + 4 * q * LY::RS];
           acc[s] = mfma4(av, buf[xrow[s] + 4 * q * LY::RS], acc[s]);
-          bsum[s] += av;
+          bsum[s] += (double)av;
         }
       }
     };
@@ -1356,8 +1360,10 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
     int ph, to, ti;
     TL::get(tau, ph, to, ti);
     if (ti == 0 && ph <= 10) {
-      const float bs = sum_groups(bsum[s]);
-      if (g == 0) bacc[(ph == 0 ? 0 : 16 + 32 * (ph - 1)) + 16 * to + i] = bs;
+      double bs = bsum[s];
+      bs += __shfl_xor(bs, 16);
+      bs += __shfl_xor(bs, 32);
+      if (g == 0) bacc[(ph == 0 ? 0 : 16 + 32 * (ph - 1)) + 16 * to + i] = (float)bs;
     }
   }
   // ---- flush: every weight-gradient element is owned by exactly one lane and

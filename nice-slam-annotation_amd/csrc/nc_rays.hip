@@ -772,7 +772,9 @@ constexpr int PR_COLS = 32, PR_PARTS = 8;
 constexpr int PR_AHEAD = NC_PR_AHEAD;  // slab rows in flight per thread (8 / 12: no gain, profiles/r04/ray_loads/ab_pr.log)
 static_assert(PR_COLS * PR_PARTS == 64 * RAY_WAVES, "k_param_ray_reduce: one block size for both roles");
 __device__ __forceinline__ void param_reduce_body(const ParamReduceCtx& c, int bx, int j) {
-  __shared__ float4 part[PR_PARTS][PR_COLS];
+  // the per-workgroup partials are summed in float64 (rounded once at the end): bias
+  // gradients cancel heavily across workgroups (k_mlp_dw's float64 bias sums)
+  __shared__ double part[PR_PARTS][PR_COLS][4];
   // constant-index selects (dynamic indexing of the argument block spills it)
   const Job job = j == 0 ? c.jobs[0] : (j == 1 ? c.jobs[1] : c.jobs[2]);
   float* grad = j == 0 ? c.grad[0] : (j == 1 ? c.grad[1] : c.grad[2]);
@@ -781,7 +783,7 @@ __device__ __forceinline__ void param_reduce_body(const ParamReduceCtx& c, int b
   const int col = threadIdx.x % PR_COLS, prt = threadIdx.x / PR_COLS;
   const int64_t e = ((int64_t)bx * PR_COLS + col) * 4;  // first parameter of the column
   if ((int64_t)bx * PR_COLS * 4 >= np) return;          // whole workgroup past the end
-  float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
   if (e < c.slab_stride) {  // slab rows are padded to slab_stride (multiple of 64 floats)
     const int w0 = j == 0 ? c.wg_off[0] : (j == 1 ? c.wg_off[1] : c.wg_off[2]);
     const int w1 = j == 0 ? c.wg_off[1] : (j == 1 ? c.wg_off[2] : c.wg_off[3]);
@@ -796,27 +798,26 @@ __device__ __forceinline__ void param_reduce_body(const ParamReduceCtx& c, int b
       for (int u = 0; u < PR_AHEAD; ++u) v[u] = row(w + u * PR_PARTS);
 #pragma unroll
       for (int u = 0; u < PR_AHEAD; ++u) {
-        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+        acc[0] += v[u].x; acc[1] += v[u].y; acc[2] += v[u].z; acc[3] += v[u].w;
       }
     }
     for (; w < nw; w += PR_PARTS) {
       const float4 v = row(w);
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
     }
   }
-  part[prt][col] = acc;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) part[prt][col][k] = acc[k];
   __syncthreads();
   if (prt == 0) {
-    float4 s4 = part[0][col];
+    double sv[4] = {part[0][col][0], part[0][col][1], part[0][col][2], part[0][col][3]};
 #pragma unroll
-    for (int q = 1; q < PR_PARTS; ++q) {
-      const float4 v = part[q][col];
-      s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
-    }
-    const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+    for (int q = 1; q < PR_PARTS; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sv[k] += part[q][col][k];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (e + k < np) grad[e + k] = sv[k];
+      if (e + k < np) grad[e + k] = (float)sv[k];
   }
 }
 

@@ -170,7 +170,7 @@ def score_vs_truth(got, ref32, ref64, out_floor=2e-5, grad_floor=2e-4):
 # ref_k: float32 computations of the same program -- ref_0 the reference's own vectors
 #    (golden cases) or the float32 oracle, ref_1.. the float32 oracle with the rays in another
 #    order (other summation orders of every reduction over points);
-# the floor: 4x the reference's own RMS float32 error over the tensor -- below 1e-6 of the
+# the floor: 4x the reference's own RMS float32 error over the tensor's non-zero elements -- below 1e-6 of the
 #    tensor's max for the large tensors, above it where float32 itself is that far off (the
 #    reference's own max error reaches 5.6e-6 of max on the golden decoder gradients).
 # Grid gradients must also have the support of ref_0: the same voxels non-zero.
@@ -197,7 +197,9 @@ def elementwise_vs_truth(got, refs, truth, factor=ELEM_FACTOR):
         ers = [(r[k].double().reshape(-1) - t).abs() for r in refs]
         er = torch.stack(ers).amax(0)
         scale = max(float(t.abs().max()), 1e-300)
-        floor = factor * float(ers[0].pow(2).mean().sqrt())
+        live = t != 0  # the RMS over the elements the reference computes (an untouched voxel's
+        #                zero gradient is exact in every implementation and would dilute it)
+        floor = factor * float(ers[0][live].pow(2).mean().sqrt()) if bool(live.any()) else 0.0
         eh = (h - t).abs()
         ratio = eh / (factor * er + max(floor, 1e-300))
         nt = float(t.norm()) or 1e-300

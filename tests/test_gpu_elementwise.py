@@ -11,8 +11,8 @@ t: the oracle in float64 keeping the reference's float32 input roundings (p.floa
 float32 lookup coordinates) -- the exact value of the reference's float32 program;
 ref_0: the reference's own vectors (tests/golden, produced by importing /root/reference)
 for the golden and init-std cases, the float32 oracle for the C2 benchmark workload;
-ref_1: the float32 oracle with the rays in reverse order (every reduction over points in
-another order).  The floor, 4x the reference's own RMS error over the tensor, is far
+ref_1, ref_2: the float32 oracle with the rays in reverse and in a random order (every
+reduction over points in other orders).  The floor, 4x the reference's own RMS error over the tensor, is far
 below the tensor's max (a voxel's wrong gradient shows unless it is within float32 noise).
 Grid gradients must also have ref_0's support: the same voxels with a non-zero gradient
 (a dropped or mis-addressed scatter of any size shows there).  The C2 workload is scored
@@ -51,10 +51,22 @@ def test_golden_elementwise(case, channels_last):
             (rec["g_depth"], rec["g_var"], rec["g_color"]))
     truth = oracle_render_grads(*args, f64=True, round_inputs=True)
     truth = {k: v for k, v in truth.items() if k in rec}  # the tensors the reference produced
-    rev = oracle_render_grads(*args, order=torch.arange(rec["rays_o"].shape[0] - 1, -1, -1))
-    res = elementwise_vs_truth(got, [rec, rev], truth)
+    n = rec["rays_o"].shape[0]
+    rev = oracle_render_grads(*args, order=torch.arange(n - 1, -1, -1))
+    perm = oracle_render_grads(*args, order=torch.randperm(n, generator=torch.Generator().manual_seed(1)))
+    res = elementwise_vs_truth(got, [rec, rev, perm], truth)
+    _dump(f"golden_{case}_{int(channels_last)}", got, [rec, rev, perm], truth)
     bad = report_elementwise(f"{case} {'channels_last' if channels_last else 'ncdhw'}", res)
     assert not bad, bad
+
+
+def _dump(name, got, refs, truth):
+    """NICECORE_ELEM_DUMP=<dir>: save the compared tensors (for offline study of the gate)."""
+    import os
+    d = os.environ.get("NICECORE_ELEM_DUMP")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        torch.save({"got": got, "refs": refs, "truth": truth}, os.path.join(d, name + ".pt"))
 
 
 def _c2_eager_and_graphed():
@@ -89,14 +101,16 @@ def test_c2_workload_elementwise_eager_and_graphed():
     render + loss + backward, per element; and the two HIP forms against each other."""
     import bench
     w, out = _c2_eager_and_graphed()
-    rev = torch.arange(w["ro"].shape[0] - 1, -1, -1)
-    f32, f32r, t64 = (False, False, None), (False, False, rev), (True, True, None)
-    refs = oracle_mapper_refs(w, bench.LOSS_KW["ba"]("color"), forms=(f32, f32r, t64))
+    n = w["ro"].shape[0]
+    rev, perm = torch.arange(n - 1, -1, -1), torch.randperm(n, generator=torch.Generator().manual_seed(1))
+    f32, f32r, f32p, t64 = (False, False, None), (False, False, rev), (False, False, perm), (True, True, None)
+    refs = oracle_mapper_refs(w, bench.LOSS_KW["ba"]("color"), forms=(f32, f32r, f32p, t64))
     bad = {}
     for form in ("eager", "graphed"):
         truth = refs[t64] if form == "eager" else {k: v for k, v in refs[t64].items()
                                                    if k not in ("depth", "var", "color")}
-        res = elementwise_vs_truth(out[form], [refs[f32], refs[f32r]], truth)
+        res = elementwise_vs_truth(out[form], [refs[f32], refs[f32r], refs[f32p]], truth)
+        _dump(f"c2_{form}", out[form], [refs[f32], refs[f32r], refs[f32p]], truth)
         bad.update({f"{form}:{k}": v for k, v in report_elementwise(f"C2 {form}", res).items()})
     # the replayed step against the eager one: ray and parameter gradients bit-identical
     # (fixed-order reductions), grid gradients to float-atomic order

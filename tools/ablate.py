@@ -13,8 +13,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "nice-slam-annotation_amd"))
 DBG = os.path.join(REPO, "dbg")
 VARIANTS = {
-    "base": [],
+    "ref": [],
     "cur": [],
+    "no_gather": ["-DNC_ABL_NO_GATHER"],
     "no_trig": ["-DNC_ABL_NO_TRIG"],
     "no_recstore": ["-DNC_ABL_NO_RECSTORE"],
     "no_mask": ["-DNC_ABL_NO_MASK"],
