@@ -1242,13 +1242,20 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
     yrow[s] = g * LY::RS + yoff;
     xrow[s] = g * LY::RS + xoff;
   }
-  // per-lane partial bias sums (rows 16*to+i), reduced once at the end: in float64, as a
-  // bias gradient is a sum over every point of the workgroup with heavy cancellation
-  // (sum_p d out_p of an occupancy decoder), where a float32 running sum over ~10^3 points
-  // was 70x less accurate than the reference's pairwise sum (tests/test_gpu_elementwise.py)
-  double bsum[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) bsum[s] = 0.0;
+  // bias gradients (column sums of dY over the points): thread e < BACC_FLOATS owns bias e
+  // (bacc order) and adds its column of every staged sub-chunk in point order, in float64.
+  // A bias gradient cancels heavily over the points (sum_p d out_p of an occupancy decoder):
+  // the former float32 per-lane sums inside the k-steps were 70x less accurate than the
+  // reference's pairwise sum (tests/test_gpu_elementwise.py), and kept NS more VGPRs live
+  int bcol = -1;  // the owned bias's column in a staged row
+  if (threadIdx.x < LY::BACC_FLOATS) {
+    const int e = threadIdx.x;
+    const int ph = e < 16 ? 0 : 1 + (e - 16) / 32, row = e < 16 ? e : (e - 16) % 32;
+    if (ph == 0) bcol = row < N::NOUT ? LY::DOUT + row : -1;
+    else if (ph <= 5) bcol = LY::DZ + HID * (5 - ph) + row;
+    else if (N::XYZ) bcol = LY::DREC + RC::DH + HID * (10 - ph) + row;
+  }
+  double bsum = 0.0;
   // ---- staging: the records of the next sub-chunk are prefetched into registers
   // (branch-free, PER float4 per thread) while the current one is consumed ----
   // A sub-chunk's records are one contiguous block of DW_NPTS * STRIDE floats: item k
@@ -1315,6 +1322,10 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
 #ifndef NC_ABL_DW_NO_LOAD  // timing-only ablation: the next records are not loaded
     if (sub + nwg < nsub) prefetch(sub + nwg);
 #endif
+    if (bcol >= 0) {  // rows past P are zero-filled: they add 0
+#pragma unroll
+      for (int r = 0; r < DW_NPTS; ++r) bsum += (double)buf[r * LY::RS + bcol];
+    }
     // ---- tiles: DW_NPTS/4 k-steps of 4 points; the wave's NS accumulation chains are
     // interleaved (k-step outer) so no MFMA waits on its predecessor's result ----
     // one k-step = NS independent MFMAs + 2 NS reads at immediate offsets; unrolled by
@@ -1332,7 +1343,6 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
         for (int s = 0; s < NC; ++s) {
           const float av = buf[yrow[s] + 4 * q * LY::RS];
           acc[s] = mfma4(av, buf[xrow[s] + 4 * q * LY::RS], acc[s]);
-          bsum[s] += (double)av;
         }
       }
     };
@@ -1352,20 +1362,7 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
       }
     }
   }
-  // bias gradients: each (phase, row block) is owned by its ti == 0 tile
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int tau = wv + DW_WAVES * s;
-    if (tau >= TL::NT) continue;
-    int ph, to, ti;
-    TL::get(tau, ph, to, ti);
-    if (ti == 0 && ph <= 10) {
-      double bs = bsum[s];
-      bs += __shfl_xor(bs, 16);
-      bs += __shfl_xor(bs, 32);
-      if (g == 0) bacc[(ph == 0 ? 0 : 16 + 32 * (ph - 1)) + 16 * to + i] = (float)bs;
-    }
-  }
+  if (bcol >= 0) bacc[threadIdx.x] = (float)bsum;
   // ---- flush: every weight-gradient element is owned by exactly one lane and
   // every bias by one bacc entry, so the slab row is written without an image ----
   float* slab = ctx.slab + (int64_t)blockIdx.x * ctx.slab_stride;  // one row per workgroup

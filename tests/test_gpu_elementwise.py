@@ -110,7 +110,6 @@ def test_c2_workload_elementwise_eager_and_graphed():
         truth = refs[t64] if form == "eager" else {k: v for k, v in refs[t64].items()
                                                    if k not in ("depth", "var", "color")}
         res = elementwise_vs_truth(out[form], [refs[f32], refs[f32r], refs[f32p]], truth)
-        _dump(f"c2_{form}", out[form], [refs[f32], refs[f32r], refs[f32p]], truth)
         bad.update({f"{form}:{k}": v for k, v in report_elementwise(f"C2 {form}", res).items()})
     # the replayed step against the eager one: ray and parameter gradients bit-identical
     # (fixed-order reductions), grid gradients to float-atomic order
