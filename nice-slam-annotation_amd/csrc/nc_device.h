@@ -165,7 +165,15 @@ __device__ __forceinline__ void mfma16_drain() {
 // slot (0..31) of feature f (0..31) inside a 32-column block: inverse of feat_of
 __host__ __device__ constexpr int hslot(int f) { return 8 * ((f >> 2) & 3) + 4 * (f >> 4) + (f & 3); }
 
-// split 8 C-layout values (one 32-feature block of a lane) into f16 hi / scaled lo
+// split 8 C-layout values (one 32-feature block of a lane) into f16 hi / scaled lo, both
+// rounded to nearest even: x = hi + 2^-11 lo to within 2^-22 relative, UNBIASED.  (Round 5:
+// the former round-toward-zero pair (v_cvt_pkrtz) truncated both halves, so every operand's
+// magnitude came out short by up to 2^-20 and 2^-21 on average -- a systematic shrink that
+// cancellation-heavy statistics accumulate: the occupancy decoders' output-bias gradient,
+// a sum of d raw over all points, was 100x further from the float64 truth than the
+// reference's float32 (tests/test_gpu_elementwise.py, profiles/r05/elementwise/).)
+// hi = RNE(x) leaves r = x - hi exact in f32 (Sterbenz: hi is within a factor 2 of x) with
+// |r| <= half an f16 ulp of x, so lo = RNE(r * 2^11) keeps 11 more bits.
 __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
 #ifdef NC_ABL_NO_SPLIT  // timing-only ablation: hi only, no lo half (results wrong)
 #pragma unroll
@@ -177,6 +185,7 @@ __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
   }
   return;
 #endif
+#ifdef NC_SPLIT_RTZ  // A/B: the round-4 truncating split
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
     const halfx2 h = __builtin_amdgcn_cvt_pkrtz(x[j], x[j + 1]);
@@ -188,6 +197,14 @@ __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
     lo[j] = (_Float16)l[0];
     lo[j + 1] = (_Float16)l[1];
   }
+#else
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)x[j];  // v_cvt_f16_f32: round to nearest even
+    hi[j] = h;
+    lo[j] = (_Float16)((x[j] - (float)h) * SPLIT_SCALE);
+  }
+#endif
 }
 
 // split8 that also folds max |x| into amax (one v_max_f32 with an |.| modifier per

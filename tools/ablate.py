@@ -79,6 +79,11 @@ VARIANTS = {
     "det_rg4": ["-DNC_DET_RG=4"],  # NC_DETERMINISTIC=1 runs
     "det_rg16": ["-DNC_DET_RG=16"],
     "no_split": ["-DNC_ABL_NO_SPLIT"],
+    "split_rtz": ["-DNC_SPLIT_RTZ"],
+    "ft2_512": ["-DNC_FWD_TILES=2", "-DNC_FWD_THREADS_FUSED=512"],
+    "ft2_768": ["-DNC_FWD_TILES=2"],
+    "ft1_512": ["-DNC_FWD_THREADS_FUSED=512"],
+    "ft1_1024": ["-DNC_FWD_THREADS_FUSED=1024"],
     "no_triw": ["-DNC_ABL_NO_TRIW"],
     "pr8": ["-DNC_PR_AHEAD=8"],
     "pr12": ["-DNC_PR_AHEAD=12"],
