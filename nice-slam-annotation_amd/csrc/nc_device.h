@@ -473,6 +473,22 @@ __device__ __forceinline__ float reduce_2pi(float x) {
   r = __builtin_fmaf(-k, 1.9353071795864769e-3f, r);
   return __builtin_fmaf(-k, 1.2537033403800354e-11f, r);
 }
+// two elements per packed-FP32 instruction (v_pk_mul_f32 / v_pk_fma_f32 on gfx950: each
+// element an IEEE mul / fma, so a packed form is bit-identical to its scalar form)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// reduce_2pi of two arguments, returned in revolutions (the argument of v_sin_f32):
+// exactly fourier_sin's reduce_2pi(x) * (1 / 2 pi), element by element
+__device__ __forceinline__ f2 fourier_arg2(f2 x) {
+  const f2 q = x * f2{0.15915494309189535f, 0.15915494309189535f};
+  const f2 k = f2{__builtin_rintf(q.x), __builtin_rintf(q.y)};
+  const f2 nk = -k;
+  f2 r = fma2(nk, f2{6.28125f, 6.28125f}, x);
+  r = fma2(nk, f2{1.9353071795864769e-3f, 1.9353071795864769e-3f}, r);
+  r = fma2(nk, f2{1.2537033403800354e-11f, 1.2537033403800354e-11f}, r);
+  return r * f2{0.15915494309189535f, 0.15915494309189535f};
+}
+
 __device__ __forceinline__ float fourier_sin(float x) {
   return __builtin_amdgcn_sinf(reduce_2pi(x) * 0.15915494309189535f);
 }

@@ -34,9 +34,11 @@
 #ifdef NC_ABL_NO_TRIG  // timing-only ablation: no trig at all
 #define NC_SIN(x) (x)
 #define NC_COS(x) (x)
+#define NC_SIN_REV(y) (y)
 #else
 #define NC_SIN fourier_sin
 #define NC_COS fourier_cos
+#define NC_SIN_REV(y) __builtin_amdgcn_sinf(y)  // sin of an argument already in revolutions (fourier_arg2)
 #endif
 
 namespace nc {
@@ -529,18 +531,26 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
     for (int t = 0; t < T; ++t) split8(R[t].c + 8 * b, ch[b][t], cl[b][t], amax);
   half8 eh[3][T], el[3][T];  // Fourier features sin(p.float() @ B), XYZ decoders
   if constexpr (N::XYZ) {
+    // two features per packed-FP32 instruction (v_pk_mul / v_pk_fma: IEEE per element, so
+    // the arguments and the reduction are bit-identical to the scalar form k_mlp_dw
+    // recomputes).  The padded B columns 93..95 are 0 in the image: sin(0) = 0 exactly.
     const float* B = F + H::FB;
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         float e[8];
+        const f2 p0 = f2{R[t].pf[0], R[t].pf[0]}, p1 = f2{R[t].pf[1], R[t].pf[1]}, p2 = f2{R[t].pf[2], R[t].pf[2]};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int m = 32 * kb + feat_of(j, g);
-          const float x = __builtin_fmaf(R[t].pf[2], B[2 * EMBP + m],
-                                         __builtin_fmaf(R[t].pf[1], B[EMBP + m], R[t].pf[0] * B[m]));
-          e[j] = (m < EMB) ? NC_SIN(x) : 0.f;
+        for (int j = 0; j < 8; j += 2) {
+          const int m = 32 * kb + feat_of(j, g);  // m + 1 = feat_of(j + 1, g)
+          const f2 b0 = *reinterpret_cast<const f2*>(B + m);
+          const f2 b1 = *reinterpret_cast<const f2*>(B + EMBP + m);
+          const f2 b2 = *reinterpret_cast<const f2*>(B + 2 * EMBP + m);
+          const f2 x = fma2(p2, b2, fma2(p1, b1, p0 * b0));
+          const f2 y = fourier_arg2(x);
+          e[j] = NC_SIN_REV(y.x);
+          e[j + 1] = NC_SIN_REV(y.y);
         }
         split8(e, eh[kb][t], el[kb][t]);
       }
@@ -553,9 +563,16 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
   for (int t = 0; t < T; ++t) mlo[t] = mhi[t] = 0;
 #pragma unroll
   for (int L = 0; L < 5; ++L) {
+    // the biases start the accumulators (z = b + W x; the fc_c output adds its own bias)
+    const float* bl = F + H::BL + L * HID;
+    const float* bc = F + H::BC + L * HID;
     floatx4 hh[T][2], mx[T][2];
 #pragma unroll
-    for (int t = 0; t < T; ++t) hh[t][0] = hh[t][1] = mx[t][0] = mx[t][1] = zero4();
+    for (int t = 0; t < T; ++t) {
+      hh[t][0] = bias4(bl, g);
+      hh[t][1] = bias4(bl + 16, g);
+      mx[t][0] = mx[t][1] = zero4();
+    }
     const char* M = img + H::lin_off(L);
     if (L == 0) {
       if constexpr (N::XYZ) {
@@ -576,28 +593,36 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
     } else {
       mac_fwd<T>(M, 0, xh, xl, hh, mx, i, g);
     }
-    const float* bl = F + H::BL + L * HID;
     floatx4 fh[T][2], fm[T][2];
     if constexpr (N::XYZ) {
 #pragma unroll
-      for (int t = 0; t < T; ++t) fh[t][0] = fh[t][1] = fm[t][0] = fm[t][1] = zero4();
+      for (int t = 0; t < T; ++t) {
+        fh[t][0] = bias4(bc, g);
+        fh[t][1] = bias4(bc + 16, g);
+        fm[t][0] = fm[t][1] = zero4();
+      }
 #pragma unroll
       for (int b = 0; b < CB; ++b) mac_fwd<T>(img + H::fc_off(L), b, ch[b], cl[b], fh, fm, i, g);
     }
-    const float* bc = F + H::BC + L * HID;
     mfma16_drain();
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       unsigned bits = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int ob = j >> 2, r = j & 3, f = 16 * ob + 4 * g + r;
-        const float z = (hh[t][ob][r] + mx[t][ob][r] * SPLIT_INV) + bl[f];
-        const bool p = z > 0.f;
-        float v = p ? z : 0.f;
-        bits |= (p ? 1u : 0u) << j;
-        if constexpr (N::XYZ) v = (v + bc[f]) + (fh[t][ob][r] + fm[t][ob][r] * SPLIT_INV);
-        h[t][j] = v;
+      for (int j = 0; j < 8; j += 2) {
+        const int ob = j >> 2, r = j & 3;
+        // z = (b + hi.hi) + 2^-11 (hi.lo + lo.hi), two features per v_pk_fma
+        const f2 z = fma2(f2{mx[t][ob][r], mx[t][ob][r + 1]}, f2{SPLIT_INV, SPLIT_INV},
+                          f2{hh[t][ob][r], hh[t][ob][r + 1]});
+        const bool p0 = z.x > 0.f, p1 = z.y > 0.f;
+        f2 v = f2{p0 ? z.x : 0.f, p1 ? z.y : 0.f};
+        bits |= (p0 ? 1u : 0u) << j;
+        bits |= (p1 ? 1u : 0u) << (j + 1);
+        if constexpr (N::XYZ)
+          v = v + fma2(f2{fm[t][ob][r], fm[t][ob][r + 1]}, f2{SPLIT_INV, SPLIT_INV},
+                       f2{fh[t][ob][r], fh[t][ob][r + 1]});
+        h[t][j] = v.x;
+        h[t][j + 1] = v.y;
       }
       if (L < 4) mlo[t] |= bits << (8 * L);
       else mhi[t] = bits;
@@ -619,10 +644,10 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
     for (int o = 0; o < 4; ++o) {
       if (o >= (KIND == K_COLOR ? 3 : 1)) { out[t][o] = 0.f; continue; }
       const float* wo = F + H::WO + o * HID;
-      float s = 0.f;
+      f2 s2 = f2{0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s = s + wo[feat_of(j, g)] * h[t][j];
-      out[t][o] = sum_groups(s) + F[H::BO + o];
+      for (int j = 0; j < 8; j += 2) s2 = fma2(*reinterpret_cast<const f2*>(wo + feat_of(j, g)), f2{h[t][j], h[t][j + 1]}, s2);
+      out[t][o] = sum_groups(s2.x + s2.y) + F[H::BO + o];
     }
   }
 }
@@ -773,6 +798,155 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
   }
 }
 
+// ---------------------------------------------------------------------------
+// Warp-specialised fused forward (round 5, NC_FWD_WS, the default for channels-last grids):
+// the trilinear lookups (MLP.sample_grid_feature, decoder.py:179-188) move out of the MLP
+// waves.  Measured on the single-role kernel: with its corner loads removed (timing
+// ablation no_gather) k_mlp_fwd ran 47.7-51.6 us instead of 73-75 -- each wave waited for
+// its tile's lookups before every MLP, all twelve in step after the weight prologue.
+// Here WS_PROD producer waves (one per SIMD) gather 16-point tiles into an LDS ring and
+// WS_CONS consumer waves run the decoders on them with no global loads at all:
+//   producer p: tiles k = p, p + WS_PROD, ... of the workgroup; per tile: corners of the
+//     next tile computed while this tile's 8 (fine: 16) corner rows are in flight, weighted
+//     sum in the reference's corner order (bit-identical to the single-role kernel), then
+//     slot k % WS_RING gets the features (C layout, lane-private) and p.float(); full[slot]
+//     = k + 1 (release).  A slot is rewritten only after done[slot] = k - WS_RING + 1.
+//   consumer: takes the next tile from an LDS counter, waits for full[slot] == k + 1
+//     (acquire), copies the features to registers, marks done, runs wave_forward_h.
+// No barrier after the roles split; every wait is a bounded spin (s_sleep), and a wave that
+// gives up raises the job's range flag, so k_mlp_fwd_exact recomputes the job on the exact
+// path -- a lost wake-up costs time, never a hang or a wrong result.
+// ---------------------------------------------------------------------------
+#ifndef NC_FWD_WS_PROD
+#define NC_FWD_WS_PROD 4
+#endif
+#ifndef NC_FWD_WS_RING
+#define NC_FWD_WS_RING 12
+#endif
+__host__ __device__ constexpr int imax_(int a, int b) { return a > b ? a : b; }
+// the split-f16 weight image of the largest decoder (floats, 16-byte aligned): the ring follows it
+constexpr int FWD_LDS_FLOATS_H =
+    ((imax_(imax_(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), imax_(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4) + 3) & ~3;
+constexpr int WS_PROD = NC_FWD_WS_PROD;
+constexpr int WS_RING = NC_FWD_WS_RING;
+constexpr int WS_CD_MAX = 64;                          // fine: [fine | middle]
+constexpr int WS_ROW = WS_CD_MAX + 4;                  // floats per point row (+4: bank spread)
+constexpr int WS_SLOT = 16 * WS_ROW + 16 * 4;          // features + p.float() of 16 points
+constexpr int WS_LDS_FLOATS = WS_RING * WS_SLOT + 2 * WS_RING + 4;  // ring, full/done flags, counter
+constexpr unsigned WS_SPIN_CAP = 1u << 21;
+static_assert(WS_RING % WS_PROD == 0, "a ring slot must always belong to the same producer");
+
+__device__ __forceinline__ bool ws_wait_ge(const int* flag, int want) {
+  for (unsigned it = 0; it < WS_SPIN_CAP; ++it) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+template <int KIND>
+__device__ __forceinline__ void fwd_job_ws(const MlpCtx& ctx, const Job& job, int j, float* lds, int64_t wg,
+                                           int64_t nwg, bool zero_fill) {
+  constexpr int CQ = Net<KIND>::CD / 16;
+  constexpr int CD = Net<KIND>::CD;
+  constexpr int NT = fwd_threads(true);
+  float* ring = lds + FWD_LDS_FLOATS_H;
+  int* full = reinterpret_cast<int*>(ring + WS_RING * WS_SLOT);
+  int* done = full + WS_RING;
+  int* ctr = done + WS_RING;
+  for (int e = threadIdx.x; e < 2 * WS_RING + 1; e += NT) full[e] = 0;  // full, done, counter
+  float amax = 0.f;
+  load_weights_h<KIND, NT>(reinterpret_cast<char*>(lds), ctx.dec[KIND], amax);  // ends with a barrier
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nblk = (ctx.P + 15) / 16;  // 16-point tiles of the job
+  const int K = wg < nblk ? (int)((nblk - wg + nwg - 1) / nwg) : 0;  // this workgroup's tiles
+  auto tile_point = [&](int k) { return (wg + (int64_t)k * nwg) * 16 + i; };
+  bool ok = true;
+  if (wave < WS_PROD) {
+    // ---- producer ----
+    const nc_grid& G = ctx.grids[KIND];
+    auto coords = [&](int k, float4& x, float4& pf) {
+      const int64_t p = tile_point(k);
+      const bool in = k < K && p < ctx.P;
+      x = in ? ctx.xyz[(int64_t)job.slot * ctx.P + p] : float4{0.f, 0.f, 0.f, 0.f};
+      pf = in ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
+    };
+    float4 nx, npf;
+    coords(wave, nx, npf);
+    for (int k = wave; k < K; k += WS_PROD) {
+      const float xyz[3] = {nx.x, nx.y, nx.z};
+      const float4 pf = npf;
+      float c[CD / 4];
+      if constexpr (KIND == K_FINE) {  // [fine | middle]: + the no-grad grid_middle lookup
+        Corners c1, c2;
+        make_corners(ctx.grids[K_FINE], xyz, c1);
+        make_corners(ctx.grids[K_MID], xyz, c2);
+        gather8x2(ctx.grids[K_FINE], c1, ctx.grids[K_MID], c2, g, c, c + 8);
+      } else {
+        Corners co;
+        make_corners(G, xyz, co);
+        gather8<true>(G, co, g, c);
+      }
+      coords(k + WS_PROD, nx, npf);  // in flight while this tile waits for its slot
+      const int sl = k % WS_RING;
+      ok = ok && ws_wait_ge(done + sl, k - WS_RING + 1);
+      float* row = ring + sl * WS_SLOT + i * WS_ROW;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q)
+        *reinterpret_cast<float4*>(row + 16 * q + 4 * g) = float4{c[4 * q + 0], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]};
+      if (g == 0) *reinterpret_cast<float4*>(ring + sl * WS_SLOT + 16 * WS_ROW + 4 * i) = pf;
+      __hip_atomic_store(full + sl, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else {
+    // ---- consumer ----
+    for (;;) {
+      int k = 0;
+      if (lane == 0) k = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      k = __builtin_amdgcn_readfirstlane(k);
+      if (k >= K) break;
+      const int sl = k % WS_RING;
+      ok = ok && ws_wait_ge(full + sl, k + 1);
+      WaveIn<KIND> R[1];
+      const float* row = ring + sl * WS_SLOT + i * WS_ROW;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(row + 16 * q + 4 * g);
+        R[0].c[4 * q + 0] = v.x; R[0].c[4 * q + 1] = v.y; R[0].c[4 * q + 2] = v.z; R[0].c[4 * q + 3] = v.w;
+      }
+      const float4 pf = *reinterpret_cast<const float4*>(ring + sl * WS_SLOT + 16 * WS_ROW + 4 * i);
+      R[0].pf[0] = pf.x; R[0].pf[1] = pf.y; R[0].pf[2] = pf.z;
+      if (lane == 0) __hip_atomic_store(done + sl, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int64_t p = tile_point(k);
+      float* rec[1];
+#ifdef NC_ABL_NO_RECSTORE
+      rec[0] = nullptr;
+#else
+      rec[0] = (ctx.save_rec && p < ctx.P) ? ctx.rec + job.rec_off + p * Rec<KIND>::STRIDE : nullptr;
+#endif
+      if (rec[0]) store_rows<CQ>(rec[0] + Rec<KIND>::C, R[0].c, g);
+      float out[1][4];
+      wave_forward_h<KIND, 1>(reinterpret_cast<const char*>(lds), i, g, R, out, rec, job.keep_h != 0, amax);
+      if (p < ctx.P && g == 0) {
+        if constexpr (KIND == K_COLOR) {
+          ctx.rgb[p * 3 + 0] = out[0][0];
+          ctx.rgb[p * 3 + 1] = out[0][1];
+          ctx.rgb[p * 3 + 2] = out[0][2];
+        } else {
+          ctx.occ[(int64_t)job.slot * ctx.P + p] = out[0][0];
+        }
+      }
+    }
+  }
+  // out of the f16 range, or a spin that gave up: the exact pass recomputes the whole job
+  if ((!(amax < RANGE_LIMIT) || !ok) && ctx.range_flag) ctx.range_flag[j] = 1u;
+  if (zero_fill && ctx.zero_fill) {  // the backward's gradient buffer (nc_render_args.grad_zero)
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t z = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; z < ctx.zero_n4; z += nthr)
+      ctx.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 // job of workgroup b in a 1-D grid split [off[0], off[1]), [off[1], off[2]), ...
 __device__ __forceinline__ int job_of_wg(const int32_t (&off)[MAX_JOBS + 1], int b) {
   return (b >= off[1] ? 1 : 0) + (b >= off[2] ? 1 : 0);
@@ -794,6 +968,17 @@ __device__ __forceinline__ void fwd_kernel(const MlpCtx& ctx, float* lds) {
   const Job job = pick_job(ctx.jobs, j);
   const int o0 = j == 0 ? ctx.fwd_off[0] : (j == 1 ? ctx.fwd_off[1] : ctx.fwd_off[2]);
   const int o1 = j == 0 ? ctx.fwd_off[1] : (j == 1 ? ctx.fwd_off[2] : ctx.fwd_off[3]);
+#ifndef NC_FWD_NO_WS
+  if constexpr (FUSE && !F32 && !EXACT) {
+    switch (job.kind) {
+      case K_COARSE: fwd_job_ws<K_COARSE>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
+      case K_MID: fwd_job_ws<K_MID>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
+      case K_FINE: fwd_job_ws<K_FINE>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
+      default: fwd_job_ws<K_COLOR>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
+    }
+    return;
+  }
+#endif
   switch (job.kind) {
     case K_COARSE: fwd_job<K_COARSE, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
     case K_MID: fwd_job<K_MID, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
@@ -1756,7 +1941,14 @@ constexpr int DW_LDS_FLOATS = cmax(cmax(DwImg<K_COARSE>::TOTAL, DwImg<K_MID>::TO
 static_assert(FWD_LDS_FLOATS * 4 <= 160 * 1024, "weight image LDS budget");
 static_assert(DW_LDS_FLOATS * 4 <= 160 * 1024, "dW staging LDS budget");
 
+#ifndef NC_FWD_NO_WS
+constexpr int FWD_FUSED_LDS_FLOATS = FWD_F32 ? FWD_LDS_FLOATS : FWD_LDS_FLOATS_H + WS_LDS_FLOATS;
+#else
+constexpr int FWD_FUSED_LDS_FLOATS = FWD_LDS_FLOATS;
+#endif
+static_assert(FWD_FUSED_LDS_FLOATS * 4 <= 160 * 1024, "weight image + producer ring LDS budget");
 int mlp_fwd_lds_bytes() { return FWD_LDS_FLOATS * 4; }
+int mlp_fwd_fused_lds_bytes() { return FWD_FUSED_LDS_FLOATS * 4; }
 int mlp_fwd_exact_lds_bytes() { return FWD_F32_LDS_FLOATS * 4; }
 int mlp_dw_lds_bytes() { return DW_LDS_FLOATS * 4; }
 int64_t max_param_count() {
@@ -1800,8 +1992,8 @@ int mlp_blocks_per_cu(int which) {
       set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<false>, FWD_THREADS, mlp_fwd_lds_bytes());
     } else if (which == 3) {
-      set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes());
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<true>, FWD_THREADS_FUSED, mlp_fwd_lds_bytes());
+      set_lds(k_mlp_fwd<true>, mlp_fwd_fused_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<true>, FWD_THREADS_FUSED, mlp_fwd_fused_lds_bytes());
     } else if (which == 1) {
       set_lds(k_mlp_dx<true, false>, mlp_dx_lds_bytes());
       set_lds(k_mlp_dx<false, false>, mlp_dx_lds_bytes());
@@ -1850,7 +2042,7 @@ constexpr int EXACT_WGS_PER_JOB = NC_EXACT_WGS;
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
   static int attr = -1;
   if (attr != 0 && (attr = set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes()) |
-                           set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes())) != 0)
+                           set_lds(k_mlp_fwd<true>, mlp_fwd_fused_lds_bytes())) != 0)
     return attr;
   static int attr_x = -1;
   if (attr_x != 0 && (attr_x = set_lds(k_mlp_fwd_exact<false>, mlp_fwd_exact_lds_bytes()) |
@@ -1858,7 +2050,7 @@ int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
     return attr_x;
   const dim3 grid(c.fwd_off[c.n_jobs]);
   if (c.fuse_gather)
-    hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(FWD_THREADS_FUSED), mlp_fwd_lds_bytes(), s, c);
+    hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(FWD_THREADS_FUSED), mlp_fwd_fused_lds_bytes(), s, c);
   else
     hipLaunchKernelGGL(k_mlp_fwd<false>, grid, dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
   if (hipError_t e = hipGetLastError()) return (int)e;
