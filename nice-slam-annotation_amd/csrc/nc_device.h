@@ -142,6 +142,19 @@ constexpr int HROW = 128;  // bytes per image row: 32 hi + 32 lo halves, chunks 
 
 // byte offset inside a row of chunk g (0..3) of plane p (0 hi, 1 lo)
 __host__ __device__ constexpr int hchunk(int row, int g, int p) { return 16 * ((g + 4 * p) ^ ((row >> 1) & 7)); }
+// The forward's weights carry a third plane (round 5): W = hi + 2^-11 (mid + lo3), all
+// round-to-nearest f16, represents a float32 weight to within 3e-11 absolute (lo3 = the
+// residual after mid, f16 subnormal for small weights), i.e. below float32's own rounding
+// for every |W| > 1e-3; lo3 . xh goes into the same 2^-11 accumulator as mid . xh.
+// With two planes each weight was off by up to 2^-22 of itself: one fixed perturbation of
+// the network, the same at every point, so its effect on sums over points did not average
+// out -- the occupancy decoders' output-bias gradient (sum of d raw) was 8x further from
+// the float64 truth than the reference's float32 in a reordered summation
+// (tests/test_gpu_elementwise.py).  Activations keep two planes: their 2^-22 rounding is
+// per point, like float32's.  lo3 rows are 64 B (chunk g of row r at g ^ ((r >> 2) & 3):
+// a 16-lane group of ds_read_b128 reading rows 0..15 touches 16 distinct 16-B bank slots).
+constexpr int HROW3 = 64;
+__host__ __device__ constexpr int hchunk3(int row, int g) { return 16 * (g ^ ((row >> 2) & 3)); }
 
 __device__ __forceinline__ floatx4 mfma16(half8 a, half8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -243,7 +256,15 @@ struct NetH {
     return o;
   }
   __host__ __device__ static constexpr int fc_off(int L) { return lin_off(5) + L * N::CD * HROW; }
-  static constexpr int BYTES = fc_off(N::NFC);
+  // third planes (HROW3-byte rows), same row order, after every two-plane matrix
+  static constexpr int B3 = fc_off(N::NFC);
+  __host__ __device__ static constexpr int lin3_off(int L) {
+    int o = B3;
+    for (int k = 0; k < L; ++k) o += kin(k) * HROW3;
+    return o;
+  }
+  __host__ __device__ static constexpr int fc3_off(int L) { return lin3_off(5) + L * N::CD * HROW3; }
+  static constexpr int BYTES = fc3_off(N::NFC);
 };
 
 // ---------------------------------------------------------------------------

@@ -144,9 +144,13 @@ __device__ __forceinline__ void load_weights(float* lds, const nc_decoder_params
 template <int KIND>
 __device__ __forceinline__ int hpos(int m, int o, int c, int plane) {  // byte offset of W_m[o][packed c]
   using H = NetH<KIND>;
-  const int base = m < 5 ? H::lin_off(m) : H::fc_off(m - 5);
   const int row = (c >> 5) * 32 + o;
   const int s = hslot(c & 31);
+  if (plane == 2) {  // the third plane
+    const int base3 = m < 5 ? H::lin3_off(m) : H::fc3_off(m - 5);
+    return base3 + row * HROW3 + hchunk3(row, s >> 3) + 2 * (s & 7);
+  }
+  const int base = m < 5 ? H::lin_off(m) : H::fc_off(m - 5);
   return base + row * HROW + hchunk(row, s >> 3, plane) + 2 * (s & 7);
 }
 
@@ -200,9 +204,17 @@ __device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_param
         const int o = e / in, c = e - o * in, cp = lin ? N::pack_col(m, c) : c;
         const float v = regs.v[k];
         amax = fmaxf(amax, fabsf(v));    // split-f16 range guard (RANGE_LIMIT)
-        const _Float16 h = (_Float16)v;  // hi / scaled lo halves of one weight
+        // three round-to-nearest planes: v = h + 2^-11 (md + l3) (the residuals are exact in
+        // f32: Sterbenz, then a power-of-two scaling); l3 = r1 - md lies in the f16 subnormal
+        // range for small weights, where its 2^-24 spacing is 2^-35 of the weight's scale:
+        // v is represented to within 3e-11 absolute, below float32's own rounding for |v| > 1e-3
+        const _Float16 h = (_Float16)v;
+        const float r1 = (v - (float)h) * SPLIT_SCALE;
+        const _Float16 md = (_Float16)r1;
+        const _Float16 l3 = (_Float16)(r1 - (float)md);
         *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 0)) = h;
-        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 1)) = (_Float16)((v - (float)h) * SPLIT_SCALE);
+        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 1)) = md;
+        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 2)) = l3;
       }
     }
   };
@@ -223,21 +235,29 @@ __device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_param
 }
 
 // acc (output rows 16 ob + 4g + r) += M[:, block kb] x, both 16-row output blocks,
-// T tiles sharing the weight fragments (forward image rows kb*32 + o)
+// T tiles sharing the weight fragments (forward image rows kb*32 + o; M3: the third planes):
+// hh += Wh xh, mx += Wh xl + (Wm + W3) xh (units 2^-11)
 template <int T>
-__device__ __forceinline__ void mac_fwd(const char* M, int kb, const half8 (&xh)[T], const half8 (&xl)[T],
-                                        floatx4 (&hh)[T][2], floatx4 (&mx)[T][2], int i, int g) {
+__device__ __forceinline__ void mac_fwd(const char* M, const char* M3, int kb, const half8 (&xh)[T],
+                                        const half8 (&xl)[T], floatx4 (&hh)[T][2], floatx4 (&mx)[T][2],
+                                        int i, int g) {
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
     const int r = kb * 32 + ob * 16 + i;
     const char* row = M + r * HROW;
     const half8 wh = *reinterpret_cast<const half8*>(row + hchunk(r, g, 0));
     const half8 wl = *reinterpret_cast<const half8*>(row + hchunk(r, g, 1));
+#ifndef NC_FWD_W2  // A/B: the round-4 two-plane weights
+    const half8 w3 = *reinterpret_cast<const half8*>(M3 + r * HROW3 + hchunk3(r, g));
+#endif
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       hh[t][ob] = mfma16(wh, xh[t], hh[t][ob]);
       mx[t][ob] = mfma16(wh, xl[t], mx[t][ob]);
       mx[t][ob] = mfma16(wl, xh[t], mx[t][ob]);
+#ifndef NC_FWD_W2
+      mx[t][ob] = mfma16(w3, xh[t], mx[t][ob]);
+#endif
     }
   }
 }
@@ -574,24 +594,25 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
       mx[t][0] = mx[t][1] = zero4();
     }
     const char* M = img + H::lin_off(L);
+    const char* M3 = img + H::lin3_off(L);
     if (L == 0) {
       if constexpr (N::XYZ) {
 #pragma unroll
-        for (int kb = 0; kb < 3; ++kb) mac_fwd<T>(M, kb, eh[kb], el[kb], hh, mx, i, g);
+        for (int kb = 0; kb < 3; ++kb) mac_fwd<T>(M, M3, kb, eh[kb], el[kb], hh, mx, i, g);
       } else {
-        mac_fwd<T>(M, 0, ch[0], cl[0], hh, mx, i, g);
+        mac_fwd<T>(M, M3, 0, ch[0], cl[0], hh, mx, i, g);
       }
     } else if (L == 3) {
       if constexpr (N::XYZ) {
 #pragma unroll
-        for (int kb = 0; kb < 3; ++kb) mac_fwd<T>(M, kb, eh[kb], el[kb], hh, mx, i, g);
-        mac_fwd<T>(M, 3, h2h, h2l, hh, mx, i, g);
+        for (int kb = 0; kb < 3; ++kb) mac_fwd<T>(M, M3, kb, eh[kb], el[kb], hh, mx, i, g);
+        mac_fwd<T>(M, M3, 3, h2h, h2l, hh, mx, i, g);
       } else {
-        mac_fwd<T>(M, 0, ch[0], cl[0], hh, mx, i, g);
-        mac_fwd<T>(M, 1, h2h, h2l, hh, mx, i, g);
+        mac_fwd<T>(M, M3, 0, ch[0], cl[0], hh, mx, i, g);
+        mac_fwd<T>(M, M3, 1, h2h, h2l, hh, mx, i, g);
       }
     } else {
-      mac_fwd<T>(M, 0, xh, xl, hh, mx, i, g);
+      mac_fwd<T>(M, M3, 0, xh, xl, hh, mx, i, g);
     }
     floatx4 fh[T][2], fm[T][2];
     if constexpr (N::XYZ) {
@@ -602,7 +623,8 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
         fm[t][0] = fm[t][1] = zero4();
       }
 #pragma unroll
-      for (int b = 0; b < CB; ++b) mac_fwd<T>(img + H::fc_off(L), b, ch[b], cl[b], fh, fm, i, g);
+      for (int b = 0; b < CB; ++b)
+        mac_fwd<T>(img + H::fc_off(L), img + H::fc3_off(L), b, ch[b], cl[b], fh, fm, i, g);
     }
     mfma16_drain();
 #pragma unroll
@@ -611,7 +633,7 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
         const int ob = j >> 2, r = j & 3;
-        // z = (b + hi.hi) + 2^-11 (hi.lo + lo.hi), two features per v_pk_fma
+        // z = (b + hi.hi) + 2^-11 (hi.lo + (mid + lo3).hi), two features per v_pk_fma
         const f2 z = fma2(f2{mx[t][ob][r], mx[t][ob][r + 1]}, f2{SPLIT_INV, SPLIT_INV},
                           f2{hh[t][ob][r], hh[t][ob][r + 1]});
         const bool p0 = z.x > 0.f, p1 = z.y > 0.f;
@@ -798,155 +820,6 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
   }
 }
 
-// ---------------------------------------------------------------------------
-// Warp-specialised fused forward (round 5, NC_FWD_WS, the default for channels-last grids):
-// the trilinear lookups (MLP.sample_grid_feature, decoder.py:179-188) move out of the MLP
-// waves.  Measured on the single-role kernel: with its corner loads removed (timing
-// ablation no_gather) k_mlp_fwd ran 47.7-51.6 us instead of 73-75 -- each wave waited for
-// its tile's lookups before every MLP, all twelve in step after the weight prologue.
-// Here WS_PROD producer waves (one per SIMD) gather 16-point tiles into an LDS ring and
-// WS_CONS consumer waves run the decoders on them with no global loads at all:
-//   producer p: tiles k = p, p + WS_PROD, ... of the workgroup; per tile: corners of the
-//     next tile computed while this tile's 8 (fine: 16) corner rows are in flight, weighted
-//     sum in the reference's corner order (bit-identical to the single-role kernel), then
-//     slot k % WS_RING gets the features (C layout, lane-private) and p.float(); full[slot]
-//     = k + 1 (release).  A slot is rewritten only after done[slot] = k - WS_RING + 1.
-//   consumer: takes the next tile from an LDS counter, waits for full[slot] == k + 1
-//     (acquire), copies the features to registers, marks done, runs wave_forward_h.
-// No barrier after the roles split; every wait is a bounded spin (s_sleep), and a wave that
-// gives up raises the job's range flag, so k_mlp_fwd_exact recomputes the job on the exact
-// path -- a lost wake-up costs time, never a hang or a wrong result.
-// ---------------------------------------------------------------------------
-#ifndef NC_FWD_WS_PROD
-#define NC_FWD_WS_PROD 4
-#endif
-#ifndef NC_FWD_WS_RING
-#define NC_FWD_WS_RING 12
-#endif
-__host__ __device__ constexpr int imax_(int a, int b) { return a > b ? a : b; }
-// the split-f16 weight image of the largest decoder (floats, 16-byte aligned): the ring follows it
-constexpr int FWD_LDS_FLOATS_H =
-    ((imax_(imax_(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), imax_(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4) + 3) & ~3;
-constexpr int WS_PROD = NC_FWD_WS_PROD;
-constexpr int WS_RING = NC_FWD_WS_RING;
-constexpr int WS_CD_MAX = 64;                          // fine: [fine | middle]
-constexpr int WS_ROW = WS_CD_MAX + 4;                  // floats per point row (+4: bank spread)
-constexpr int WS_SLOT = 16 * WS_ROW + 16 * 4;          // features + p.float() of 16 points
-constexpr int WS_LDS_FLOATS = WS_RING * WS_SLOT + 2 * WS_RING + 4;  // ring, full/done flags, counter
-constexpr unsigned WS_SPIN_CAP = 1u << 21;
-static_assert(WS_RING % WS_PROD == 0, "a ring slot must always belong to the same producer");
-
-__device__ __forceinline__ bool ws_wait_ge(const int* flag, int want) {
-  for (unsigned it = 0; it < WS_SPIN_CAP; ++it) {
-    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-
-template <int KIND>
-__device__ __forceinline__ void fwd_job_ws(const MlpCtx& ctx, const Job& job, int j, float* lds, int64_t wg,
-                                           int64_t nwg, bool zero_fill) {
-  constexpr int CQ = Net<KIND>::CD / 16;
-  constexpr int CD = Net<KIND>::CD;
-  constexpr int NT = fwd_threads(true);
-  float* ring = lds + FWD_LDS_FLOATS_H;
-  int* full = reinterpret_cast<int*>(ring + WS_RING * WS_SLOT);
-  int* done = full + WS_RING;
-  int* ctr = done + WS_RING;
-  for (int e = threadIdx.x; e < 2 * WS_RING + 1; e += NT) full[e] = 0;  // full, done, counter
-  float amax = 0.f;
-  load_weights_h<KIND, NT>(reinterpret_cast<char*>(lds), ctx.dec[KIND], amax);  // ends with a barrier
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int64_t nblk = (ctx.P + 15) / 16;  // 16-point tiles of the job
-  const int K = wg < nblk ? (int)((nblk - wg + nwg - 1) / nwg) : 0;  // this workgroup's tiles
-  auto tile_point = [&](int k) { return (wg + (int64_t)k * nwg) * 16 + i; };
-  bool ok = true;
-  if (wave < WS_PROD) {
-    // ---- producer ----
-    const nc_grid& G = ctx.grids[KIND];
-    auto coords = [&](int k, float4& x, float4& pf) {
-      const int64_t p = tile_point(k);
-      const bool in = k < K && p < ctx.P;
-      x = in ? ctx.xyz[(int64_t)job.slot * ctx.P + p] : float4{0.f, 0.f, 0.f, 0.f};
-      pf = in ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
-    };
-    float4 nx, npf;
-    coords(wave, nx, npf);
-    for (int k = wave; k < K; k += WS_PROD) {
-      const float xyz[3] = {nx.x, nx.y, nx.z};
-      const float4 pf = npf;
-      float c[CD / 4];
-      if constexpr (KIND == K_FINE) {  // [fine | middle]: + the no-grad grid_middle lookup
-        Corners c1, c2;
-        make_corners(ctx.grids[K_FINE], xyz, c1);
-        make_corners(ctx.grids[K_MID], xyz, c2);
-        gather8x2(ctx.grids[K_FINE], c1, ctx.grids[K_MID], c2, g, c, c + 8);
-      } else {
-        Corners co;
-        make_corners(G, xyz, co);
-        gather8<true>(G, co, g, c);
-      }
-      coords(k + WS_PROD, nx, npf);  // in flight while this tile waits for its slot
-      const int sl = k % WS_RING;
-      ok = ok && ws_wait_ge(done + sl, k - WS_RING + 1);
-      float* row = ring + sl * WS_SLOT + i * WS_ROW;
-#pragma unroll
-      for (int q = 0; q < CQ; ++q)
-        *reinterpret_cast<float4*>(row + 16 * q + 4 * g) = float4{c[4 * q + 0], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]};
-      if (g == 0) *reinterpret_cast<float4*>(ring + sl * WS_SLOT + 16 * WS_ROW + 4 * i) = pf;
-      __hip_atomic_store(full + sl, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  } else {
-    // ---- consumer ----
-    for (;;) {
-      int k = 0;
-      if (lane == 0) k = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      k = __builtin_amdgcn_readfirstlane(k);
-      if (k >= K) break;
-      const int sl = k % WS_RING;
-      ok = ok && ws_wait_ge(full + sl, k + 1);
-      WaveIn<KIND> R[1];
-      const float* row = ring + sl * WS_SLOT + i * WS_ROW;
-#pragma unroll
-      for (int q = 0; q < CQ; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(row + 16 * q + 4 * g);
-        R[0].c[4 * q + 0] = v.x; R[0].c[4 * q + 1] = v.y; R[0].c[4 * q + 2] = v.z; R[0].c[4 * q + 3] = v.w;
-      }
-      const float4 pf = *reinterpret_cast<const float4*>(ring + sl * WS_SLOT + 16 * WS_ROW + 4 * i);
-      R[0].pf[0] = pf.x; R[0].pf[1] = pf.y; R[0].pf[2] = pf.z;
-      if (lane == 0) __hip_atomic_store(done + sl, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const int64_t p = tile_point(k);
-      float* rec[1];
-#ifdef NC_ABL_NO_RECSTORE
-      rec[0] = nullptr;
-#else
-      rec[0] = (ctx.save_rec && p < ctx.P) ? ctx.rec + job.rec_off + p * Rec<KIND>::STRIDE : nullptr;
-#endif
-      if (rec[0]) store_rows<CQ>(rec[0] + Rec<KIND>::C, R[0].c, g);
-      float out[1][4];
-      wave_forward_h<KIND, 1>(reinterpret_cast<const char*>(lds), i, g, R, out, rec, job.keep_h != 0, amax);
-      if (p < ctx.P && g == 0) {
-        if constexpr (KIND == K_COLOR) {
-          ctx.rgb[p * 3 + 0] = out[0][0];
-          ctx.rgb[p * 3 + 1] = out[0][1];
-          ctx.rgb[p * 3 + 2] = out[0][2];
-        } else {
-          ctx.occ[(int64_t)job.slot * ctx.P + p] = out[0][0];
-        }
-      }
-    }
-  }
-  // out of the f16 range, or a spin that gave up: the exact pass recomputes the whole job
-  if ((!(amax < RANGE_LIMIT) || !ok) && ctx.range_flag) ctx.range_flag[j] = 1u;
-  if (zero_fill && ctx.zero_fill) {  // the backward's gradient buffer (nc_render_args.grad_zero)
-    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t z = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; z < ctx.zero_n4; z += nthr)
-      ctx.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
-  }
-}
-
 // job of workgroup b in a 1-D grid split [off[0], off[1]), [off[1], off[2]), ...
 __device__ __forceinline__ int job_of_wg(const int32_t (&off)[MAX_JOBS + 1], int b) {
   return (b >= off[1] ? 1 : 0) + (b >= off[2] ? 1 : 0);
@@ -968,17 +841,6 @@ __device__ __forceinline__ void fwd_kernel(const MlpCtx& ctx, float* lds) {
   const Job job = pick_job(ctx.jobs, j);
   const int o0 = j == 0 ? ctx.fwd_off[0] : (j == 1 ? ctx.fwd_off[1] : ctx.fwd_off[2]);
   const int o1 = j == 0 ? ctx.fwd_off[1] : (j == 1 ? ctx.fwd_off[2] : ctx.fwd_off[3]);
-#ifndef NC_FWD_NO_WS
-  if constexpr (FUSE && !F32 && !EXACT) {
-    switch (job.kind) {
-      case K_COARSE: fwd_job_ws<K_COARSE>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
-      case K_MID: fwd_job_ws<K_MID>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
-      case K_FINE: fwd_job_ws<K_FINE>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
-      default: fwd_job_ws<K_COLOR>(ctx, job, j, lds, b - o0, o1 - o0, true); break;
-    }
-    return;
-  }
-#endif
   switch (job.kind) {
     case K_COARSE: fwd_job<K_COARSE, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
     case K_MID: fwd_job<K_MID, FUSE, F32>(ctx, job, j, lds, b - o0, o1 - o0, !EXACT); break;
@@ -1941,14 +1803,7 @@ constexpr int DW_LDS_FLOATS = cmax(cmax(DwImg<K_COARSE>::TOTAL, DwImg<K_MID>::TO
 static_assert(FWD_LDS_FLOATS * 4 <= 160 * 1024, "weight image LDS budget");
 static_assert(DW_LDS_FLOATS * 4 <= 160 * 1024, "dW staging LDS budget");
 
-#ifndef NC_FWD_NO_WS
-constexpr int FWD_FUSED_LDS_FLOATS = FWD_F32 ? FWD_LDS_FLOATS : FWD_LDS_FLOATS_H + WS_LDS_FLOATS;
-#else
-constexpr int FWD_FUSED_LDS_FLOATS = FWD_LDS_FLOATS;
-#endif
-static_assert(FWD_FUSED_LDS_FLOATS * 4 <= 160 * 1024, "weight image + producer ring LDS budget");
 int mlp_fwd_lds_bytes() { return FWD_LDS_FLOATS * 4; }
-int mlp_fwd_fused_lds_bytes() { return FWD_FUSED_LDS_FLOATS * 4; }
 int mlp_fwd_exact_lds_bytes() { return FWD_F32_LDS_FLOATS * 4; }
 int mlp_dw_lds_bytes() { return DW_LDS_FLOATS * 4; }
 int64_t max_param_count() {
@@ -1992,8 +1847,8 @@ int mlp_blocks_per_cu(int which) {
       set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes());
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<false>, FWD_THREADS, mlp_fwd_lds_bytes());
     } else if (which == 3) {
-      set_lds(k_mlp_fwd<true>, mlp_fwd_fused_lds_bytes());
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<true>, FWD_THREADS_FUSED, mlp_fwd_fused_lds_bytes());
+      set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes());
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp_fwd<true>, FWD_THREADS_FUSED, mlp_fwd_lds_bytes());
     } else if (which == 1) {
       set_lds(k_mlp_dx<true, false>, mlp_dx_lds_bytes());
       set_lds(k_mlp_dx<false, false>, mlp_dx_lds_bytes());
@@ -2042,7 +1897,7 @@ constexpr int EXACT_WGS_PER_JOB = NC_EXACT_WGS;
 int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
   static int attr = -1;
   if (attr != 0 && (attr = set_lds(k_mlp_fwd<false>, mlp_fwd_lds_bytes()) |
-                           set_lds(k_mlp_fwd<true>, mlp_fwd_fused_lds_bytes())) != 0)
+                           set_lds(k_mlp_fwd<true>, mlp_fwd_lds_bytes())) != 0)
     return attr;
   static int attr_x = -1;
   if (attr_x != 0 && (attr_x = set_lds(k_mlp_fwd_exact<false>, mlp_fwd_exact_lds_bytes()) |
@@ -2050,7 +1905,7 @@ int launch_mlp_fwd(const MlpCtx& c, hipStream_t s) {
     return attr_x;
   const dim3 grid(c.fwd_off[c.n_jobs]);
   if (c.fuse_gather)
-    hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(FWD_THREADS_FUSED), mlp_fwd_fused_lds_bytes(), s, c);
+    hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(FWD_THREADS_FUSED), mlp_fwd_lds_bytes(), s, c);
   else
     hipLaunchKernelGGL(k_mlp_fwd<false>, grid, dim3(FWD_THREADS), mlp_fwd_lds_bytes(), s, c);
   if (hipError_t e = hipGetLastError()) return (int)e;

@@ -80,9 +80,7 @@ VARIANTS = {
     "det_rg16": ["-DNC_DET_RG=16"],
     "no_split": ["-DNC_ABL_NO_SPLIT"],
     "split_rtz": ["-DNC_SPLIT_RTZ"],
-    "no_ws": ["-DNC_FWD_NO_WS"],
-    "ws_r16": ["-DNC_FWD_WS_RING=16"],
-    "ws_p2": ["-DNC_FWD_WS_PROD=2"],
+    "fwd_w2": ["-DNC_FWD_W2"],
     "ft2_512": ["-DNC_FWD_TILES=2", "-DNC_FWD_THREADS_FUSED=512"],
     "ft2_768": ["-DNC_FWD_TILES=2"],
     "ft1_512": ["-DNC_FWD_THREADS_FUSED=512"],
