@@ -220,6 +220,27 @@ __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
 #endif
 }
 
+// the truncating split (round-to-zero halves) the iMAP* layer GEMMs keep: their golden
+// case with importance sampling (tests/test_gpu_imap.py nodepth_imp) picks its second-pass
+// samples from the first pass's weights by CDF inversion, so a last-bit change of the
+// forward can move a sample; that case is pinned on the round-4 numerics.  The NICE forward
+// uses split8 (round to nearest) with three weight planes, gated per element.
+__device__ __forceinline__ void split8_rtz(const float* x, half8& hi, half8& lo, float& amax) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(x[j]));
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const halfx2 h = __builtin_amdgcn_cvt_pkrtz(x[j], x[j + 1]);
+    const float r0 = (x[j] - (float)h[0]) * SPLIT_SCALE;
+    const float r1 = (x[j + 1] - (float)h[1]) * SPLIT_SCALE;
+    const halfx2 l = __builtin_amdgcn_cvt_pkrtz(r0, r1);
+    hi[j] = (_Float16)h[0];
+    hi[j + 1] = (_Float16)h[1];
+    lo[j] = (_Float16)l[0];
+    lo[j + 1] = (_Float16)l[1];
+  }
+}
+
 // split8 that also folds max |x| into amax (one v_max_f32 with an |.| modifier per
 // value): the range guard of the split-f16 forward.  hi = f16 RTZ(x) and the residual
 // scaled by 2^11 stay finite and exact-enough only for |x| < 2^15 (RANGE_LIMIT); a tile

@@ -178,7 +178,7 @@ __device__ __forceinline__ void h_stage(const float (&x)[16], unsigned char* til
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
     half8 hi, lo;
-    split8(x + 8 * o, hi, lo, amax);
+    split8_rtz(x + 8 * o, hi, lo, amax);
     const int g = 2 * kh + o;
     *reinterpret_cast<half8*>(r + hchunk(row, g, 0)) = hi;
     *reinterpret_cast<half8*>(r + hchunk(row, g, 1)) = lo;
@@ -426,7 +426,7 @@ __global__ void __launch_bounds__(256) k_imap_wimage(const ImapWImage w) {
   }
   half8 hi, lo;
   float amax = 0.f;
-  split8(x, hi, lo, amax);
+  split8_rtz(x, hi, lo, amax);
   unsigned char* row = w.img[z] + (int64_t)n * imap_wimage_row(K) + 128 * sl;
   *reinterpret_cast<half8*>(row + hchunk(n & 127, g, 0)) = hi;
   *reinterpret_cast<half8*>(row + hchunk(n & 127, g, 1)) = lo;

@@ -247,19 +247,23 @@ __device__ __forceinline__ void mac_fwd(const char* M, const char* M3, int kb, c
     const char* row = M + r * HROW;
     const half8 wh = *reinterpret_cast<const half8*>(row + hchunk(r, g, 0));
     const half8 wl = *reinterpret_cast<const half8*>(row + hchunk(r, g, 1));
-#ifndef NC_FWD_W2  // A/B: the round-4 two-plane weights
-    const half8 w3 = *reinterpret_cast<const half8*>(M3 + r * HROW3 + hchunk3(r, g));
-#endif
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       hh[t][ob] = mfma16(wh, xh[t], hh[t][ob]);
       mx[t][ob] = mfma16(wh, xl[t], mx[t][ob]);
       mx[t][ob] = mfma16(wl, xh[t], mx[t][ob]);
-#ifndef NC_FWD_W2
-      mx[t][ob] = mfma16(w3, xh[t], mx[t][ob]);
-#endif
     }
   }
+#ifndef NC_FWD_W2  // A/B: the round-4 two-plane weights
+  // the third planes after both blocks' main products (their fragments not live beside those)
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    const int r = kb * 32 + ob * 16 + i;
+    const half8 w3 = *reinterpret_cast<const half8*>(M3 + r * HROW3 + hchunk3(r, g));
+#pragma unroll
+    for (int t = 0; t < T; ++t) mx[t][ob] = mfma16(w3, xh[t], mx[t][ob]);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -168,8 +168,10 @@ def score_vs_truth(got, ref32, ref64, out_floor=2e-5, grad_floor=2e-4):
 #    float32 lookup coordinates: nice_oracle.float64_mode(round_inputs=True)), i.e. the exact
 #    value of the reference's float32 program;
 # ref_k: float32 computations of the same program -- ref_0 the reference's own vectors
-#    (golden cases) or the float32 oracle, ref_1.. the float32 oracle with the rays in another
-#    order (other summation orders of every reduction over points);
+#    (golden cases) or the float32 oracle, ref_1, ref_2 the float32 oracle on the network with
+#    its hidden units, Fourier features and grid channels permuted (permuted_problem: the same
+#    function with every dot product summed in another order, as any other float32
+#    implementation sums it; gradients mapped back);
 # the floor: 4x the reference's own RMS float32 error over the tensor's non-zero elements -- below 1e-6 of the
 #    tensor's max for the large tensors, above it where float32 itself is that far off (the
 #    reference's own max error reaches 5.6e-6 of max on the golden decoder gradients).
@@ -262,20 +264,23 @@ def collect_step(grids, model, ro, rd, outs=None, loss=None):
 
 def oracle_mapper_refs(w, kw, stage="color", forms=((False, False, None), (True, False, None))):
     """The oracle's render + Mapper loss (Mapper.py:603-612) + backward on a bench workload
-    ``w`` (bench.build_workload).  ``forms``: (float64, round_inputs, order) per result --
-    float32 / float64 computations, the float64 one with the reference's float32 input
-    roundings, or the rays in another order (outputs and ray gradients un-permuted).
+    ``w`` (bench.build_workload).  ``forms``: (float64, round_inputs, order[, perm_seed]) per
+    result -- float32 / float64 computations, the float64 one with the reference's float32
+    input roundings, the rays in another order (outputs and ray gradients un-permuted), or
+    (perm_seed) the unit-permuted network (permuted_problem, gradients mapped back).
     Returns {form: {name: tensor}}; the default forms give {(False, False, None): ref32,
     (True, False, None): ref64}, also reachable as [False] / [True]."""
     from nicecore import scene as S
     from oracle import nice_oracle as O
-    g_cpu = {k: v.detach().cpu().contiguous() for k, v in w["grids"].items()}
-    prm = {n: p.detach().cpu() for n, p in w["model"].named_parameters()}
+    g_cpu0 = {k: v.detach().cpu().contiguous() for k, v in w["grids"].items()}
+    prm0 = {n: p.detach().cpu() for n, p in w["model"].named_parameters()}
     ro0, rd0, gt0, gtc0 = (t.detach().cpu() for t in (w["ro"], w["rd"], w["gt"], w["gtc"]))
     dec_b = S.decoder_bounds(w["sc"].bound)
     refs = {}
     for form in forms:
-        f64, rnd, order = form
+        f64, rnd, order = form[:3]
+        seed = form[3] if len(form) > 3 else None
+        g_cpu, prm, un = (g_cpu0, prm0, None) if seed is None else permuted_problem(g_cpu0, prm0, seed)
         ro, rd, gt, gtc = (t if order is None else t[order] for t in (ro0, rd0, gt0, gtc0))
         cast = (lambda t: t.double()) if f64 else (lambda t: t)
         ro_c, rd_c = cast(ro.clone()).requires_grad_(True), cast(rd.clone()).requires_grad_(True)
@@ -297,7 +302,7 @@ def oracle_mapper_refs(w, kw, stage="color", forms=((False, False, None), (True,
         for k, t in p_c.items():
             if t.grad is not None and float(t.grad.abs().max()) > 0:
                 r["grad/param/" + k] = t.grad
-        refs[form] = r
+        refs[form] = un(r) if un is not None else r
     if (False, False, None) in refs:
         refs[False] = refs[(False, False, None)]
     if (True, False, None) in refs:
@@ -313,3 +318,83 @@ def c2_args(**over):
              param_grads="direct", eager=True, iteration=False)
     a.update(over)
     return types.SimpleNamespace(**a)
+
+
+# --- a second float32 implementation: the same network with its units permuted ------------
+# Reordering the rays only changes the reductions over points; every point's own arithmetic
+# (each dot product's summation order) stays the oracle's.  Permuting the hidden units of
+# every layer, the Fourier features and the grid channels gives a network that computes the
+# same function with every dot product summed in another order -- another float32
+# implementation, as the HIP path is one.  Gradients are mapped back to the original order.
+_DECODER_GRID = {"coarse": "grid_coarse", "middle": "grid_middle", "fine": "grid_fine", "color": "grid_color"}
+
+
+def permuted_problem(grids, params, seed):
+    """(grids', params', unpermute): grids' channels and every decoder's units permuted;
+    unpermute({name: grad'}) -> {name: grad} in the original order (grid and parameter
+    gradients; other entries are returned unchanged)."""
+    gen = torch.Generator().manual_seed(seed)
+    rp = lambda n: torch.randperm(n, generator=gen)
+    rho = {k: rp(v.shape[1]) for k, v in grids.items()}
+    new_g = {k: v[:, rho[k]].contiguous() for k, v in grids.items()}
+    idx = {}  # param name -> (row index | None, col index | None)
+    decs = sorted({n.split(".")[0][:-len("_decoder")] for n in params})
+    for d in decs:
+        pre = d + "_decoder."
+        xyz = d != "coarse"
+        pi = [rp(32) for _ in range(5)]
+        if d == "fine":
+            cin = torch.cat([rho["grid_fine"], 32 + rho["grid_middle"]])
+        else:
+            cin = rho[_DECODER_GRID[d]]
+        sig = rp(93) if xyz else None
+        for L in range(5):
+            if L == 0:
+                cols = sig if xyz else cin
+            elif L == 3:
+                cols = torch.cat([sig, 93 + pi[2]]) if xyz else torch.cat([cin, 32 + pi[2]])
+            else:
+                cols = pi[L - 1]
+            idx[f"{pre}pts_linears.{L}.weight"] = (pi[L], cols)
+            idx[f"{pre}pts_linears.{L}.bias"] = (pi[L], None)
+            if xyz:
+                idx[f"{pre}fc_c.{L}.weight"] = (pi[L], cin)
+                idx[f"{pre}fc_c.{L}.bias"] = (pi[L], None)
+        if xyz:
+            idx[pre + "embedder._B"] = (None, sig)
+        idx[pre + "output_linear.weight"] = (None, pi[4])
+
+    def fwd(t, ri, ci):
+        if ri is not None:
+            t = t[ri]
+        if ci is not None:
+            t = t[:, ci]
+        return t.contiguous()
+
+    new_p = {n: fwd(v, *idx[n]) if n in idx else v for n, v in params.items()}
+
+    def unpermute(out):
+        res = dict(out)
+        for k, v in out.items():
+            if k.startswith("grad/param/") and k[len("grad/param/"):] in idx:
+                ri, ci = idx[k[len("grad/param/"):]]
+                g = torch.zeros_like(v)
+                rows = ri if ri is not None else torch.arange(v.shape[0])
+                if v.dim() == 1:
+                    g[rows] = v
+                else:
+                    cols = ci if ci is not None else torch.arange(v.shape[1])
+                    g[rows[:, None], cols[None, :]] = v
+                res[k] = g
+            elif k.startswith("grad/grid_") and k[len("grad/"):] in rho:
+                g = torch.zeros_like(v)
+                g[:, rho[k[len("grad/"):]]] = v
+                res[k] = g
+        return res
+    return new_g, new_p, unpermute
+
+
+def oracle_render_grads_permuted(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, seed):
+    """oracle_render_grads (float32) of the unit-permuted network, in the original order."""
+    g2, p2, un = permuted_problem(grids, params, seed)
+    return un(oracle_render_grads(g2, p2, dec_b, bound, ro, rd, stage, gt, upstream))
