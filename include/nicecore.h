@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define NC_ABI_VERSION 10
+#define NC_ABI_VERSION 11
 #define NC_MAX_SAMPLES 64 /* n_strat + n_surf per ray (one wavefront per ray) */
 #define NC_MAX_SURF 32
 
@@ -280,7 +280,14 @@ typedef struct nc_sample_args {
   /* backward */
   const void* g_rays_o;      /* [F*n][3] pose dtype, NULL = 0 */
   const void* g_rays_d;      /* [F*n][3] pose dtype, NULL = 0 */
-  void* g_c2w;               /* [F][3][4] contiguous, pose dtype (written) */
+  void* g_c2w;               /* [F][3][4] contiguous, pose dtype (written), or NULL with g_cam */
+  /* ABI v11: the Tracker's camera tensor instead of c2w (src/common.py:163-176
+   * get_camera_from_tensor: [qr, qi, qj, qk, tx, ty, tz] -> [quad2rotation(q) | t], with
+   * two_s = 2 / |q|^2, common.py:137-160), so that a tracking iteration needs no torch ops
+   * between the optimiser's camera tensor and the rays; the backward then writes d cam. */
+  const void* cam;           /* [F][7] pose dtype, or NULL (then c2w) */
+  int64_t cam_stride[2];     /* frame, element strides */
+  void* g_cam;               /* [F][7] contiguous, pose dtype (written by the backward when cam) */
 } nc_sample_args;
 
 int nc_sample_rays_forward(const nc_sample_args* args, void* stream);

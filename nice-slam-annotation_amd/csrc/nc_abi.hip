@@ -1028,8 +1028,9 @@ static int sample_check(const nc_sample_args* a) {
   if (a->pose_dtype != NC_POSE_F32 && a->pose_dtype != NC_POSE_F64) return fail(-1, "nicecore: unknown pose dtype");
   if (a->n_frames < 0 || a->n_per_frame < 0) return fail(-1, "nicecore: negative frame / ray count");
   if (a->H0 < 0 || a->W0 < 0 || a->H1 <= a->H0 || a->W1 <= a->W0) return fail(-1, "nicecore: empty sampling region");
-  if (a->n_frames * a->n_per_frame > 0 && (!a->c2w || (!a->indices && !(a->pix_i && a->pix_j))))
-    return fail(-1, "nicecore: sampling needs c2w and indices (or pix_i and pix_j)");
+  if (a->n_frames * a->n_per_frame > 0 && (!(a->c2w || a->cam) || (!a->indices && !(a->pix_i && a->pix_j))))
+    return fail(-1, "nicecore: sampling needs c2w (or cam) and indices (or pix_i and pix_j)");
+  if (a->c2w && a->cam) return fail(-1, "nicecore: pass c2w or cam, not both");
   if (a->pix_i && (a->depth || a->color)) return fail(-1, "nicecore: pix_i / pix_j rays gather no depth or colour");
   return 0;
 }
@@ -1047,7 +1048,8 @@ int nc_sample_rays_forward(const nc_sample_args* a, void* stream) {
 int nc_sample_rays_backward(const nc_sample_args* a, void* stream) {
   if (int e = sample_check(a)) return e;
   if (a->n_frames == 0) return 0;
-  if (!a->g_c2w) return fail(-1, "nicecore: NULL pose gradient output");
+  if (!a->g_c2w && !(a->cam && a->g_cam)) return fail(-1, "nicecore: NULL pose gradient output");
+  if (a->cam && !a->g_cam) return fail(-1, "nicecore: NULL camera-tensor gradient output");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return check_hip(timed(KID_SAMPLE_POSE_GRAD, s, [&] { return launch_sample_pose_grad(*a, s); }), "k_sample_pose_grad");
 }

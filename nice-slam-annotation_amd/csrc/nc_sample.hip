@@ -19,8 +19,75 @@
 namespace nc {
 
 template <typename T>
-__device__ __forceinline__ T pose_at(const nc_sample_args& a, int64_t f, int r, int c) {
-  return reinterpret_cast<const T*>(a.c2w)[f * a.c2w_stride[0] + r * a.c2w_stride[1] + c * a.c2w_stride[2]];
+__device__ __forceinline__ T cam_at(const nc_sample_args& a, int64_t f, int k) {
+  return reinterpret_cast<const T*>(a.cam)[f * a.cam_stride[0] + k * a.cam_stride[1]];
+}
+
+// quad2rotation's P_ab (R_ab = 1 - s P_ab on the diagonal, s P_ab off it; s = 2 / |q|^2),
+// q = (qr, qi, qj, qk) -- src/common.py:137-160 term by term
+template <typename T>
+__device__ __forceinline__ void quad_terms(const T (&q)[4], T (&P)[3][3]) {
+  const T qr = q[0], qi = q[1], qj = q[2], qk = q[3];
+  P[0][0] = qj * qj + qk * qk; P[0][1] = qi * qj - qk * qr; P[0][2] = qi * qk + qj * qr;
+  P[1][0] = qi * qj + qk * qr; P[1][1] = qi * qi + qk * qk; P[1][2] = qj * qk - qi * qr;
+  P[2][0] = qi * qk - qj * qr; P[2][1] = qj * qk + qi * qr; P[2][2] = qi * qi + qj * qj;
+}
+
+// c2w rows 0..2 of frame f: the caller's matrix, or get_camera_from_tensor(cam[f])
+// (common.py:163-176: [quad2rotation(q) | t])
+template <typename T>
+__device__ __forceinline__ void pose_rows(const nc_sample_args& a, int64_t f, T (&M)[3][4]) {
+  if (a.cam) {
+    T q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = cam_at<T>(a, f, k);
+    const T s = (T)2 / (((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+    T P[3][3];
+    quad_terms(q, P);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) M[r][c] = r == c ? (T)1 - s * P[r][c] : s * P[r][c];
+      M[r][3] = cam_at<T>(a, f, 4 + r);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        M[r][c] = reinterpret_cast<const T*>(a.c2w)[f * a.c2w_stride[0] + r * a.c2w_stride[1] + c * a.c2w_stride[2]];
+  }
+}
+
+// d loss / d cam from d loss / d c2w (G: 3 x 4): the chain rule through quad2rotation --
+// dR_ab/dq_m = sigma_ab (ds/dq_m P_ab + s dP_ab/dq_m), ds/dq_m = -s 2 q_m / |q|^2
+template <typename T>
+__device__ __forceinline__ void cam_grad(const T (&q)[4], const T (&G)[12], T (&gc)[7]) {
+  const T n = ((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3];
+  const T s = (T)2 / n;
+  T P[3][3];
+  quad_terms(q, P);
+  const T qr = q[0], qi = q[1], qj = q[2], qk = q[3];
+  // dP_ab/dq_m for m = r, i, j, k
+  const T dP[3][3][4] = {
+      {{0, 0, 2 * qj, 2 * qk}, {-qk, qj, qi, -qr}, {qj, qk, qr, qi}},
+      {{qk, qj, qi, qr}, {0, 2 * qi, 0, 2 * qk}, {-qi, -qr, qk, qj}},
+      {{-qj, qk, -qr, qi}, {qi, qr, qk, qj}, {0, 2 * qi, 2 * qj, 0}}};
+  T gsP = 0;  // sum_ab sigma_ab G_ab P_ab
+  T gdP[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const T sg = r == c ? -G[r * 4 + c] : G[r * 4 + c];
+      gsP += sg * P[r][c];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) gdP[m] += sg * dP[r][c][m];
+    }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) gc[m] = (-s * (T)2 * q[m] / n) * gsP + s * gdP[m];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) gc[4 + r] = G[r * 4 + 3];
 }
 
 // torch.max / torch.min over a dim propagate NaN
@@ -52,14 +119,16 @@ __global__ void __launch_bounds__(256) k_sample_rays(const nc_sample_args a) {
   const float dj = -((fj - a.cy) / a.fy);
   const float dk = -1.f;
   const T d[3] = {(T)di, (T)dj, (T)dk};
+  T M[3][4];
+  pose_rows<T>(a, f, M);
   T o[3], rd[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    const T p0 = d[0] * pose_at<T>(a, f, q, 0);
-    const T p1 = d[1] * pose_at<T>(a, f, q, 1);
-    const T p2 = d[2] * pose_at<T>(a, f, q, 2);
+    const T p0 = d[0] * M[q][0];
+    const T p1 = d[1] * M[q][1];
+    const T p2 = d[2] * M[q][2];
     rd[q] = (p0 + p1) + p2;
-    o[q] = pose_at<T>(a, f, q, 3);
+    o[q] = M[q][3];
   }
   T* ro = reinterpret_cast<T*>(a.rays_o) + r * 3;
   T* rdd = reinterpret_cast<T*>(a.rays_d) + r * 3;
@@ -136,7 +205,17 @@ __global__ void __launch_bounds__(256) k_sample_pose_grad(const nc_sample_args a
     }
     __syncthreads();
   }
-  if (threadIdx.x < 12) reinterpret_cast<T*>(a.g_c2w)[f * 12 + threadIdx.x] = red[threadIdx.x][0];
+  if (a.g_c2w && threadIdx.x < 12) reinterpret_cast<T*>(a.g_c2w)[f * 12 + threadIdx.x] = red[threadIdx.x][0];
+  if (a.cam && threadIdx.x == 0) {  // d cam (get_camera_from_tensor's backward) in the same launch
+    T q[4], G[12], gc[7];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = cam_at<T>(a, f, k);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) G[k] = red[k][0];
+    cam_grad(q, G, gc);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) reinterpret_cast<T*>(a.g_cam)[f * 7 + k] = gc[k];
+  }
 }
 
 int launch_sample_rays(const nc_sample_args& a, hipStream_t s) {

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_size_t
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnicecore.so")
 
-NC_ABI_VERSION = 10
+NC_ABI_VERSION = 11
 NC_SAVE_FOR_BACKWARD = 1
 NC_DETERMINISTIC = 2
 NC_SAVE_POINT_JACOBIAN = 4
@@ -89,7 +89,7 @@ class NcSampleArgs(ctypes.Structure):
                 ("color_stride", c_int64 * 4), ("bound", c_void_p), ("rays_o", c_void_p),
                 ("rays_d", c_void_p), ("gt_depth", c_void_p), ("gt_color", c_void_p),
                 ("inside", c_void_p), ("g_rays_o", c_void_p), ("g_rays_d", c_void_p),
-                ("g_c2w", c_void_p)]
+                ("g_c2w", c_void_p), ("cam", c_void_p), ("cam_stride", c_int64 * 2), ("g_cam", c_void_p)]
 
 
 class NcFrustumArgs(ctypes.Structure):

@@ -69,8 +69,13 @@ class SampleRaysFn(torch.autograd.Function):
         a.n_frames, a.n_per_frame = F, n
         a.H0, a.H1, a.W0, a.W1 = spec["region"]
         a.fx, a.fy, a.cx, a.cy = spec["intrinsics"]
-        a.c2w = c2w_d.data_ptr()
-        _strides(a, c2w_d, "c2w_stride", 3)
+        ctx.cam = spec.get("cam", False)
+        if ctx.cam:  # [F, 7] camera tensors (ABI v11): get_camera_from_tensor inside the kernels
+            a.cam = c2w_d.data_ptr()
+            _strides(a, c2w_d, "cam_stride", 2)
+        else:
+            a.c2w = c2w_d.data_ptr()
+            _strides(a, c2w_d, "c2w_stride", 3)
         keep = [c2w_d]
         if indices is not None:
             indices = indices.to(device=device, dtype=torch.int64).contiguous()
@@ -130,9 +135,14 @@ class SampleRaysFn(torch.autograd.Function):
         gd = g_d.detach().to(c2w.dtype).contiguous() if g_d is not None else None
         a.g_rays_o = go.data_ptr() if go is not None else None
         a.g_rays_d = gd.data_ptr() if gd is not None else None
+        stream = L.raw_stream(c2w.device)
+        if ctx.cam:  # d cam written by the pose-gradient launch itself
+            gcam = torch.empty(c2w.shape[0], 7, device=c2w.device, dtype=c2w.dtype)
+            a.g_cam, a.g_c2w = gcam.data_ptr(), None
+            L.check(lib.nc_sample_rays_backward(ctypes.byref(a), stream), "nc_sample_rays_backward")
+            return None, gcam, None, None, None, None, None, None
         g34 = torch.empty(c2w.shape[0], 3, 4, device=c2w.device, dtype=c2w.dtype)
         a.g_c2w = g34.data_ptr()
-        stream = L.raw_stream(c2w.device)
         L.check(lib.nc_sample_rays_backward(ctypes.byref(a), stream), "nc_sample_rays_backward")
         if ctx.c2w_shape[1] == 3:
             g = g34
@@ -166,6 +176,30 @@ def sample_frames(H0, H1, W0, W1, n, fx, fy, cx, cy, c2w, depth=None, color=None
             torch.empty(0, n, dtype=torch.int64, device=device)
     spec = {"n": n, "region": (H0, H1, W0, W1), "intrinsics": (fx, fy, cx, cy), "bound": bound}
     return SampleRaysFn.apply(spec, c2w, indices, None, None, depth, color, frame_ids)
+
+
+def sample_frames_from_tensor(H0, H1, W0, W1, n, fx, fy, cx, cy, camera_tensor, depth=None, color=None,
+                              frame_ids=None, bound=None, indices=None, device=None):
+    """sample_frames for the Tracker's camera tensor(s) [F, 7] or [7] ([qr, qi, qj, qk, tx, ty,
+    tz]): get_camera_from_tensor (common.py:163-176) is evaluated inside the sampling kernel
+    and its backward inside the pose-gradient kernel (ABI v11), so a tracking iteration's
+    camera -> rays -> render -> loss -> d camera chain is library launches only (no torch
+    quaternion ops and their autograd nodes).  Same returns as sample_frames; the rays
+    backpropagate into ``camera_tensor``."""
+    cam = camera_tensor if isinstance(camera_tensor, torch.Tensor) else torch.as_tensor(camera_tensor)
+    if cam.dim() == 1:
+        cam = cam.unsqueeze(0)
+    if cam.dim() != 2 or cam.shape[1] != 7:
+        raise L.NiceCoreError("camera tensors must be [7] or [F, 7]")
+    device = cam.device if device is None else torch.device(device)
+    cam = cam.to(device)
+    F = cam.shape[0]
+    if indices is None:
+        region = (H1 - H0) * (W1 - W0)
+        indices = torch.stack([torch.randint(region, (n,), device=device) for _ in range(F)]) if F else \
+            torch.empty(0, n, dtype=torch.int64, device=device)
+    spec = {"n": n, "region": (H0, H1, W0, W1), "intrinsics": (fx, fy, cx, cy), "bound": bound, "cam": True}
+    return SampleRaysFn.apply(spec, cam, indices, None, None, depth, color, frame_ids)
 
 
 def get_samples(H0, H1, W0, W1, n, H, W, fx, fy, cx, cy, c2w, depth, color, device, indices=None):

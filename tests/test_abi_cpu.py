@@ -168,7 +168,7 @@ def test_sample_args_validated(lib):
     assert b"region" in lib.nc_last_error()
     a.H1 = 4
     assert lib.nc_sample_rays_forward(ctypes.byref(a), None) < 0
-    assert b"c2w and indices" in lib.nc_last_error()
+    assert b"needs c2w" in lib.nc_last_error() and b"and indices" in lib.nc_last_error()
     a.c2w, a.indices = 8, 8
     assert lib.nc_sample_rays_forward(ctypes.byref(a), None) < 0
     assert b"ray outputs" in lib.nc_last_error()

@@ -156,3 +156,46 @@ def test_hip_frames_batch_and_prefilter():
     ro_c, rd_c, _, _ = NS.bbox_filter(ro, rd, d, c, inside)
     ((ro_c * wo.cuda()).sum() + (rd_c * wd.cuda()).sum()).backward()
     assert rel(c2w_g.grad.cpu(), c2w_o.grad) <= 1e-5
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_hip_camera_tensor_sampling(dtype):
+    """sample_frames_from_tensor (ABI v11): get_camera_from_tensor (common.py:163-176) inside
+    the sampling kernel and its backward inside the pose-gradient kernel, against the
+    reference's torch ops (oracle.sampling_oracle.camera_from_tensor) feeding sample_frames:
+    rays to float rounding, the camera-tensor gradient to 1e-5 of max-abs -- with quaternions
+    off unit norm (two_s = 2 / |q|^2), as Adam leaves them, and several frames."""
+    from nicecore import sampling as NS
+    gen = torch.Generator().manual_seed(21)
+    K, F, H, W, n = 3, 3, 30, 40, 300
+    fx, fy, cx, cy = 35.0, 35.0, 19.5, 14.5
+    depths = (torch.rand(K, H, W, generator=gen) * 3).cuda()
+    colors = torch.rand(K, H, W, 3, generator=gen).cuda()
+    cam = torch.cat([torch.randn(F, 4, generator=gen) * 0.7, torch.rand(F, 3, generator=gen) - 0.5], 1).to(dtype)
+    bound = torch.tensor([[-1.5, 1.5], [-1.2, 1.2], [-2.0, 2.0]], dtype=torch.float64)
+    idx = torch.randint(H * W, (F, n), generator=gen).cuda()
+    fid = torch.tensor([2, 0, 1]).cuda()
+    up_o, up_d = (torch.randn(F * n, 3, generator=gen, dtype=dtype).cuda() for _ in range(2))
+    # the reference's ops
+    c1 = cam.cuda().requires_grad_(True)
+    ro1, rd1, d1, col1, in1 = NS.sample_frames(0, H, 0, W, n, fx, fy, cx, cy, SO.camera_from_tensor(c1), depths,
+                                               colors, frame_ids=fid, bound=bound, indices=idx)
+    ((ro1 * up_o).sum() + (rd1 * up_d).sum()).backward()
+    # fused
+    c2 = cam.cuda().requires_grad_(True)
+    ro2, rd2, d2, col2, in2 = NS.sample_frames_from_tensor(0, H, 0, W, n, fx, fy, cx, cy, c2, depths, colors,
+                                                           frame_ids=fid, bound=bound, indices=idx)
+    ((ro2 * up_o).sum() + (rd2 * up_d).sum()).backward()
+    tol = 1e-6 if dtype == torch.float32 else 1e-13
+    assert rel(ro2.detach().cpu(), ro1.detach().cpu()) <= tol and rel(rd2.detach().cpu(), rd1.detach().cpu()) <= tol
+    assert torch.equal(d1, d2) and torch.equal(col1, col2)
+    assert int((in1 != in2).sum()) <= 1  # a ray exactly on the filter's edge may flip with the last bit
+    assert rel(c2.grad.cpu(), c1.grad.cpu()) <= (1e-5 if dtype == torch.float32 else 1e-12)
+    # one camera as a [7] tensor, the Tracker's form
+    c3 = cam[0].cuda().requires_grad_(True)
+    ro3, rd3, _, _, _ = NS.sample_frames_from_tensor(0, H, 0, W, n, fx, fy, cx, cy, c3, depths, colors,
+                                                     indices=idx[:1])
+    (rd3.sum() + ro3.sum()).backward()
+    assert c3.grad.shape == (7,) and bool(torch.isfinite(c3.grad).all())

@@ -90,22 +90,57 @@ def graph_variant(args, r, grids, model, cam, sc, depth_d, color_d, bound, dev):
         loss.backward()
         opt_g.step()
         return loss, inside.sum()
-    step = GraphedStep(body)
-    for _ in range(args.warmup):
-        step()[0].item()
-    torch.cuda.synchronize()
-    kept_total = torch.zeros((), device=dev, dtype=torch.int64)
-    t = time.perf_counter()
-    for _ in range(args.iters):
-        loss, nk = step()
-        lg = loss.item()  # the Tracker's loss.item() sync, once per iteration
-        kept_total += nk
-    torch.cuda.synchronize()
-    g_ms = (time.perf_counter() - t) / args.iters * 1e3
-    return {"graph_ms_per_iteration": round(g_ms, 4), "graph_last_loss": lg,
-            "graph_rays_kept_frac": round(float(kept_total) / (args.iters * args.pixels), 4),
-            "mask_check": {"loss_masked": lm, "loss_compacted": lc, "camera_grad_rel_err": gerr,
-                           "rays_kept_frac": round(kept, 4)}}
+    def run(step):
+        for _ in range(args.warmup):
+            step()[0].item()
+        torch.cuda.synchronize()
+        kept_total = torch.zeros((), device=dev, dtype=torch.int64)
+        t = time.perf_counter()
+        for _ in range(args.iters):
+            loss, nk = step()
+            lg = loss.item()  # the Tracker's loss.item() sync, once per iteration
+            kept_total += nk
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / args.iters * 1e3, lg, float(kept_total) / (args.iters * args.pixels)
+
+    g_ms, lg, kf = run(GraphedStep(body))
+    out = {"graph_ms_per_iteration": round(g_ms, 4), "graph_last_loss": lg, "graph_rays_kept_frac": round(kf, 4),
+           "mask_check": {"loss_masked": lm, "loss_compacted": lc, "camera_grad_rel_err": gerr,
+                          "rays_kept_frac": round(kept, 4)}}
+    # the fused form: camera tensor -> rays inside the sampling kernel and d camera inside the
+    # pose-gradient kernel (sample_frames_from_tensor, ABI v11), the 7-float Adam as one
+    # k_adam_multi launch (nicecore.optim.Adam, capturable) -- checked first against the
+    # torch-ops form on one eager iteration from the same camera
+    from nicecore.optim import Adam as NcAdam
+    from nicecore.sampling import sample_frames_from_tensor
+    ref_cam = cam.detach().clone().requires_grad_(True)
+    fus_cam = cam.detach().clone().requires_grad_(True)
+    for cm, fused in ((ref_cam, False), (fus_cam, True)):
+        torch.manual_seed(4321)
+        if fused:
+            ro, rd, gd, gc, inside = sample_frames_from_tensor(E, H - E, E, W - E, args.pixels, sc.fx, sc.fy, sc.cx,
+                                                               sc.cy, cm, depth_d, color_d, bound=bound, device=dev)
+        else:
+            ro, rd, gd, gc, inside = sample_frames(
+                E, H - E, E, W - E, args.pixels, sc.fx, sc.fy, sc.cx, sc.cy, camera_from_tensor(cm).unsqueeze(0),
+                depth_d, color_d, bound=bound, device=dev)
+        r.render_batch_loss(grids, model, rd, ro, dev, "color", gd, gc, **kw, ray_mask=inside)[3].backward()
+    ferr = float((fus_cam.grad - ref_cam.grad).abs().max() / ref_cam.grad.abs().max().clamp_min(1e-30))
+    cam_f = cam.detach().clone().requires_grad_(True)
+    opt_f = NcAdam([cam_f], lr=1e-3, capturable=True)
+
+    def body_fused():
+        cam_f.grad = None
+        ro, rd, gd, gc, inside = sample_frames_from_tensor(E, H - E, E, W - E, args.pixels, sc.fx, sc.fy, sc.cx,
+                                                           sc.cy, cam_f, depth_d, color_d, bound=bound, device=dev)
+        d, u, c, loss = r.render_batch_loss(grids, model, rd, ro, dev, "color", gd, gc, **kw, ray_mask=inside)
+        loss.backward()
+        opt_f.step()
+        return loss, inside.sum()
+    f_ms, lf, kff = run(GraphedStep(body_fused))
+    out.update({"graph_fused_ms_per_iteration": round(f_ms, 4), "graph_fused_last_loss": lf,
+                "graph_fused_rays_kept_frac": round(kff, 4), "fused_camera_grad_rel_err_vs_torch_ops": ferr})
+    return out
 
 
 def main():
