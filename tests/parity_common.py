@@ -214,14 +214,24 @@ def elementwise_vs_truth(got, refs, truth, factor=ELEM_FACTOR):
     return res
 
 
-def grid_support_diff(got, ref):
-    """(voxels with a non-zero gradient only in ``got``, only in ``ref``) of [1, C, D, H, W]
-    grid gradients: a dropped or mis-addressed scatter shows here whatever its size.  ``ref``
-    must make the same float32 corner decisions (the float32 reference, not a float64 truth:
-    a coordinate within an ulp of a voxel plane picks other corners in float64)."""
-    a = (got.reshape(got.shape[-4], -1) != 0).any(0)
-    b = (ref.reshape(ref.shape[-4], -1) != 0).any(0)
-    return int((a & ~b).sum()), int((b & ~a).sum())
+def grid_support_diff(got, ref, tol=2.0 ** -24):
+    """(voxels with a non-zero gradient only in ``got``, only in ``ref``, the largest such
+    voxel's magnitude in units of max |ref|) of [1, C, D, H, W] grid gradients: a dropped or
+    mis-addressed scatter shows here.  A voxel counts when its magnitude (max over channels)
+    exceeds ``tol`` x max |ref| -- below float32's resolution at the tensor's scale a
+    contribution is the product of an underflowing transmittance (T = prod (1 - alpha)
+    reaches the float32 subnormals behind a surface; where it flushes to zero depends on
+    the order of the product), not an addressing decision.  ``ref`` must make the same
+    float32 corner decisions (the float32 reference, not a float64 truth: a coordinate
+    within an ulp of a voxel plane picks other corners in float64)."""
+    a = got.reshape(got.shape[-4], -1).abs().amax(0).double()
+    b = ref.reshape(ref.shape[-4], -1).abs().amax(0).double()
+    cut = tol * max(float(b.max()), 1e-300)
+    only_a, only_b = (a != 0) & (b == 0), (b != 0) & (a == 0)
+    mag = max(float(a[only_a].max()) if bool(only_a.any()) else 0.0,
+              float(b[only_b].max()) if bool(only_b.any()) else 0.0) / max(float(b.max()), 1e-300)
+    return int((only_a & (a > cut)).sum()), int((only_b & (b > cut)).sum()), mag, \
+        int(only_a.sum()), int(only_b.sum())
 
 
 def report_elementwise(title, res):
@@ -235,8 +245,9 @@ def report_elementwise(title, res):
               f"l2 {v.get('l2_hip', float('nan')):.2e} / {v.get('l2_ref', float('nan')):.2e}  "
               f"max {v.get('max_hip', float('nan')):.2e} / {v.get('max_ref', float('nan')):.2e}  "
               f"floor {v.get('floor', float('nan')):.1e}"
-              + (f"  support +{sup[0]} -{sup[1]}" if sup else ""))
-        if not v["worst"] <= 1.0 or (sup and sup != (0, 0)):
+              + (f"  support +{sup[0]} -{sup[1]} (below tol: +{sup[3] - sup[0]} -{sup[4] - sup[1]}, "
+                 f"largest {sup[2]:.1e} of max)" if sup else ""))
+        if not v["worst"] <= 1.0 or (sup and sup[:2] != (0, 0)):
             bad[k] = v
     worst = max((v["worst"] for v in res.values()), default=0.0)
     print(f"  worst per-element ratio over all tensors: {worst:.4g}")

@@ -24,12 +24,13 @@ gt = rec["gt_depth"] if wd else None
 args = (grids, params, dec_b, bound, rec["rays_o"], rec["rays_d"], stage, gt, (rec["g_depth"], rec["g_var"], rec["g_color"]))
 t = oracle_render_grads(*args, f64=True, round_inputs=True)
 lib = os.environ.get("NICECORE_LIB", "default")
-for k in ("grad/param/middle_decoder.output_linear.bias", "grad/param/color_decoder.output_linear.bias",
-          "grad/param/middle_decoder.fc_c.4.bias"):
-    if k in t:
+keys = sorted(k for k in t if k.startswith("grad/param/") and k.endswith(".bias")) + ["depth", "var"]
+for k in keys:
+    if k in t and k in got:
         tt = t[k].double()
-        print(f"{os.path.basename(lib)} {case} {k}: hip-t {((got[k].double() - tt).abs().max()):.3e}  "
-              f"ref-t {((rec[k].double() - tt).abs().max()):.3e}  |t| {tt.abs().max():.3e}")
+        m = max(float(tt.abs().max()), 1e-300)
+        print(f"{os.path.basename(lib)} {case} {k:46s}: hip-t {float((got[k].double() - tt).abs().max()) / m:.3e}  "
+              f"ref-t {float((rec[k].double() - tt).abs().max()) / m:.3e}  (of |t| {m:.3e})")
 # raw on the case's points
 if "pts" not in rec:
     sys.exit(0)
