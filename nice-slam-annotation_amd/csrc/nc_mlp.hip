@@ -1474,6 +1474,9 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
 // mask words, the Fourier features recomputed from p.float() with the forward's
 // fourier_sin.  Bias gradients are the dY rows' f32 sums, kept by their threads.
 // ---------------------------------------------------------------------------
+#ifndef NC_DW_RING
+#define NC_DW_RING 2  // record blocks in the split-f16 dW's LDS-DMA ring (3: 135 vs 131 us)
+#endif
 template <int KIND>
 struct DwImg {
   using N = Net<KIND>;
@@ -1493,11 +1496,14 @@ struct DwImg {
   static constexpr int RAW = 16 * RC::STRIDE;               // floats of one sub-chunk's records
   static constexpr int PIECES = (RAW * 4 + 1023) / 1024;    // 1-KiB LDS-DMA pieces
   static_assert(RAW * 4 == PIECES * 1024, "a sub-chunk's records are whole 1-KiB pieces");
-  // LDS (floats)
-  static constexpr int RAWB = 0;                          // [2][RAW] record blocks
-  static constexpr int IMG = RAWB + 2 * RAW;              // [2][NROWS][16]
-  static constexpr int INV = IMG + 2 * NROWS * 16;        // [2][NROWSP] 1 / s per row
-  static constexpr int FB = INV + 2 * NROWSP;             // [3][EMBP] Fourier B
+  // LDS (floats): a ring of NRAW record blocks (the LDS-DMA runs NRAW - 1 sub-chunks ahead)
+  // and one image (the barrier that opens a sub-chunk orders its build after the previous
+  // sub-chunk's MFMA reads)
+  static constexpr int NRAW = NC_DW_RING;
+  static constexpr int RAWB = 0;                          // [NRAW][RAW] record blocks
+  static constexpr int IMG = RAWB + NRAW * RAW;           // [NROWS][16]
+  static constexpr int INV = IMG + NROWS * 16;            // [NROWSP] 1 / s per row
+  static constexpr int FB = INV + NROWSP;                 // [3][EMBP] Fourier B
   static constexpr int BACC = FB + 3 * EMBP;              // bias accumulators (DwLayout order)
   static constexpr int TOTAL = BACC + DwLayout<KIND>::BACC_FLOATS;
   static_assert(NTHR <= DW_THREADS, "one image-build thread per record row, four per Fourier row");
@@ -1586,6 +1592,9 @@ __device__ __forceinline__ void dw_job_h(const MlpCtx& ctx, const Job& job, int 
   // (pieces past the block repeat the last one: identical bytes); bytes past the job's
   // last point read the block's first bytes instead (those points are masked below)
   auto stage = [&](int64_t sub, int b) {
+#ifdef NC_ABL_DWH_NO_DMA  // timing-only ablation: records not loaded
+    return;
+#endif
     const int64_t blk = sub * IM::RAW * 4;
     const int64_t valid = (ctx.P - sub * NP) * (int64_t)RC::STRIDE * 4;
 #pragma unroll
@@ -1596,11 +1605,13 @@ __device__ __forceinline__ void dw_job_h(const MlpCtx& ctx, const Job& job, int 
       glds16(recs + blk + (off < valid ? off : 0), lds_raw + (uint32_t)(b * IM::RAW * 4 + pc * 1024));
     }
   };
-  // ---- prologue ----
-  if (wg < nsub) stage(wg, 0);
+  // ---- prologue: the first NRAW - 1 sub-chunks in flight ----
+#pragma unroll
+  for (int a = 0; a < IM::NRAW - 1; ++a)
+    if (wg + a * nwg < nsub) stage(wg + a * nwg, a);
   for (int e = t; e < DwLayout<KIND>::BACC_FLOATS; e += blockDim.x) bacc[e] = 0.f;
-  if (t < 8) reinterpret_cast<float4*>(lds + IM::IMG + (t >> 2) * IM::NROWS * 16)[t & 3] = float4{0.f, 0.f, 0.f, 0.f};
-  if (t < 2) lds[IM::INV + t * IM::NROWSP] = 1.f;
+  if (t < 4) reinterpret_cast<float4*>(lds + IM::IMG)[t] = float4{0.f, 0.f, 0.f, 0.f};
+  if (t == 0) lds[IM::INV] = 1.f;
   if constexpr (N::XYZ) {
     const float* Bsrc = KIND == K_MID ? ctx.dec[K_MID].fourier_B
                         : KIND == K_FINE ? ctx.dec[K_FINE].fourier_B : ctx.dec[K_COLOR].fourier_B;
@@ -1628,20 +1639,25 @@ __device__ __forceinline__ void dw_job_h(const MlpCtx& ctx, const Job& job, int 
   floatx4 acc[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) acc[s] = zero4();
+  constexpr int SPW = (IM::PIECES + DW_WAVES - 1) / DW_WAVES;  // LDS-DMA instructions per wave and stage
+  static_assert(IM::NRAW == 2 || IM::NRAW == 3, "ring of 2 or 3 record blocks");
   int n = 0;
   for (int64_t sub = wg; sub < nsub; sub += nwg, ++n) {
-    const int b = n & 1;
-    // S1: this sub-chunk's records have landed (every wave's pieces; the barrier also
-    //     orders the last image reads of raw block b ^ 1 and image b before their reuse)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int b = n % IM::NRAW;
+    // S1: this sub-chunk's records have landed (every wave's pieces; a later sub-chunk's
+    //     stay in flight); the barrier also orders the previous sub-chunk's image reads
+    //     before this build and its raw block's reads before that block's next DMA
+    if (IM::NRAW == 3 && sub + nwg < nsub) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // S2: the next sub-chunk's records, in flight across S3-S5
-    if (sub + nwg < nsub) stage(sub + nwg, b ^ 1);
-    // S3: image b from raw block b
+    // S2: the sub-chunk NRAW - 1 ahead, in flight across the following iterations
+    if (sub + (IM::NRAW - 1) * nwg < nsub) stage(sub + (IM::NRAW - 1) * nwg, (n + IM::NRAW - 1) % IM::NRAW);
+    // S3: the image from raw block b
+#ifndef NC_ABL_DWH_NO_BUILD  // timing-only ablation: no image build
     {
       const float* raw = lds + IM::RAWB + b * IM::RAW;
-      char* img = reinterpret_cast<char*>(lds + IM::IMG + b * IM::NROWS * 16);
-      float* inv = lds + IM::INV + b * IM::NROWSP;
+      char* img = reinterpret_cast<char*>(lds + IM::IMG);
+      float* inv = lds + IM::INV;
       const int64_t np = ctx.P - sub * NP;  // valid points in this sub-chunk (>= 1)
       if (rec_row) {
         float v[NP];
@@ -1699,21 +1715,26 @@ __device__ __forceinline__ void dw_job_h(const MlpCtx& ctx, const Job& job, int 
         if (q == 0) inv[R] = 1.f / 16384.f;
       }
     }
+#endif
     // S4: the image is complete (LDS writes retired; the LDS-DMA stays in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // S5: the tiles: two MFMAs per tile over the 16 points, unscaled into the running sums
     {
-      const char* im = reinterpret_cast<const char*>(lds + IM::IMG + b * IM::NROWS * 16);
-      const float* inv = lds + IM::INV + b * IM::NROWSP;
+      const char* im = reinterpret_cast<const char*>(lds + IM::IMG);
+      const float* inv = lds + IM::INV;
       floatx4 P[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const half8 a = *reinterpret_cast<const half8*>(im + ya[s]);
         const half8 bh = *reinterpret_cast<const half8*>(im + xa[s]);
         const half8 bl = *reinterpret_cast<const half8*>(im + (xa[s] ^ 32));
+#ifndef NC_ABL_DWH_NO_MFMA  // timing-only ablation: no MFMAs
         P[s] = mfma16(a, bh, zero4());
         P[s] = mfma16(a, bl, P[s]);
+#else
+        P[s] = floatx4{(float)a[0], (float)bh[0], (float)bl[0], 0.f};
+#endif
       }
       mfma16_drain();
 #pragma unroll

@@ -68,6 +68,11 @@ VARIANTS = {
                 "-DNC_ABL_DW_NO_LOAD", "-DNC_ABL_DW_NO_MFMA"],
     "dw_serial_nomfma": ["-DNC_DW_SERIAL", "-DNC_ABL_DW_NO_MFMA"],
     "dw_split16": ["-DNC_DW_SPLIT16"],
+    "dw_split16_r3": ["-DNC_DW_SPLIT16", "-DNC_DW_RING=3"],
+    "dwh_no_build": ["-DNC_DW_SPLIT16", "-DNC_ABL_DWH_NO_BUILD"],
+    "dwh_no_dma": ["-DNC_DW_SPLIT16", "-DNC_ABL_DWH_NO_DMA"],
+    "dwh_no_mfma": ["-DNC_DW_SPLIT16", "-DNC_ABL_DWH_NO_MFMA"],
+    "dwh_none": ["-DNC_DW_SPLIT16", "-DNC_ABL_DWH_NO_BUILD", "-DNC_ABL_DWH_NO_DMA", "-DNC_ABL_DWH_NO_MFMA"],
     "fill2": ["-DNC_FILL_WGS_PER_CU=2"],
     "fill3": ["-DNC_FILL_WGS_PER_CU=3"],
     "scat_u2": ["-DNC_SCAT_UNROLL=2"],
