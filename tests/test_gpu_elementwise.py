@@ -50,6 +50,8 @@ from conftest import load_scene
 # same rel-L2), the weight representation (three planes, exact to 3e-11) and the split-f16
 # activation inputs (tools/diag_split_emulation.py: an oracle with the same input rounding
 # stays at 0.71 of the gate); the middle decoder of the same case is at the reference's level.
+# Eight other float32 implementations (unit-permuted oracles, tools/gate_spread.py) score
+# 0.48-1.07 of this gate on this 20-ray case.
 _NOISY = pytest.mark.xfail(strict=False, reason="fine decoder deep-layer gradient noise 1.5-2x float32's "
                                                 "(worst 1.14 of the gate on 1-2 elements), DESIGN.md §5")
 _GOLDEN = [pytest.param(c, marks=_NOISY) if c == "fine_depth" else c for c in CASE_NAMES + INITSTD_CASES]
