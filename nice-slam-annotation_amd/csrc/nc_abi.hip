@@ -366,7 +366,7 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
       w.dval[b] = take((size_t)ne * 4);
     }
     w.dw = take((size_t)ne * 4);
-    w.dpart = take((size_t)(ne + 31) / 32 * 2 * 32 * 4);
+    w.dpart = take((size_t)(ne + 8 * DET_DSUB - 1) / (8 * DET_DSUB) * 2 * 32 * 4);
     w.dsort_bits = det_sort_bits(vbits + 2);
     w.dtemp_bytes = det_sort_temp_bytes(ne, w.dsort_bits);
     w.dtemp = take(w.dtemp_bytes);

@@ -83,15 +83,22 @@ __global__ void __launch_bounds__(256) k_det_keys(const MlpCtx m, DetBufs d) {
   store8(d.w + e0, ww);
 }
 
-// The sorted entries are cut into sub-chunks of DSUB = 32, one per half-wave (lane =
-// channel).  A voxel's run of entries is summed in entry order, one sub-chunk at a
-// time: k_det_runs sums every run piece of its sub-chunk and writes the runs that lie
-// inside it straight to the gradient; a run that crosses a sub-chunk boundary leaves
-// its pieces in DetBufs::part (slot 0: the sub-chunk's first run, slot 1: its last), and
-// k_det_join, in the sub-chunk where the run starts, adds them up in sub-chunk order.
-// Every run has one writer, a hot voxel's thousands of entries are summed 32 at a time
+// The sorted entries are cut into sub-chunks of DSUB = 16, one per half-wave (lane =
+// channel), eight per workgroup (a chunk of DCH = 8 DSUB entries).  A voxel's run of
+// entries is summed in entry order, one sub-chunk at a time: k_det_runs sums every run
+// piece of its sub-chunk in registers and parks the sums in LDS; a run that crosses
+// sub-chunk boundaries inside the chunk is then added up, piece by piece in sub-chunk
+// order, by the half-wave where it starts, and every run that ends inside the chunk is
+// written straight to the gradient.  A run that crosses a chunk boundary leaves its
+// chunk's piece in DetBufs::part (slot 0: the chunk's first run, slot 1: its last), and
+// k_det_join, in the chunk where the run starts, adds the pieces up in chunk order.
+// Every run has one writer, a hot voxel's thousands of entries are summed 16 at a time
 // in parallel, and the order is fixed by the sort: bit-identical from run to run.
-constexpr int DSUB = 32;
+// (16-entry sub-chunks: 70 VGPRs and 17 KB of LDS, 7 waves per SIMD where 32 entries
+// held 4; the in-chunk join keeps the extra boundaries out of k_det_join.)
+constexpr int DSUB = DET_DSUB;
+constexpr int DCH = 8 * DSUB;
+static_assert(DSUB == 16 || DSUB == 32, "a sub-chunk fits one half-wave");
 
 __device__ __forceinline__ uint32_t shfl_key(uint32_t v, int src) { return __shfl(v, src, 32); }
 __device__ __forceinline__ uint64_t shfl_key(uint64_t v, int src) {
@@ -158,6 +165,8 @@ template <typename K>
 __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int64_t n) {
   __shared__ float racc[8][DSUB][32];
   __shared__ K rkey[8][DSUB];
+  __shared__ K rnext[8];  // the key after each sub-chunk (invalid past the end)
+  __shared__ int rcnt[8];  // runs of each sub-chunk
   const int hw = threadIdx.x >> 5, ch = threadIdx.x & 31;
   const int64_t s = (int64_t)blockIdx.x * 8 + hw;
   const int64_t e0 = s * DSUB;
@@ -204,11 +213,48 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
     if (ch == 0) rkey[hw][nr] = cur;
     ++nr;
   }
-  __syncthreads();
-  if (cnt == 0) return;
   const K prevk = e0 > 0 ? kprev : invalid;
   const K nextk = e0 + cnt < n ? knext : invalid;
-  float* part = d.part + s * 2 * 32 + ch;
+  if (ch == 0) {
+    rcnt[hw] = nr;
+    rnext[hw] = cnt > 0 ? nextk : invalid;
+  }
+  __syncthreads();
+  if (cnt == 0) return;
+  // runs crossing this sub-chunk's ends: the first continues an earlier run (cin), the last
+  // goes on into the next sub-chunk (cout)
+  const K kf = rkey[hw][0], kl = rkey[hw][nr - 1];
+  const bool cin = kf != invalid && prevk == kf;
+  const bool cout = kl != invalid && nextk == kl;
+  float* part = d.part + (int64_t)blockIdx.x * 2 * 32 + ch;
+  // the run continuing from the previous chunk: its pieces here, summed by half-wave 0
+  if (hw == 0 && cin) {
+    float acc = racc[0][0][ch];
+    bool open = nr == 1 && cout;
+    for (int t = 1; open && t < 8; ++t) {
+      acc = acc + racc[t][0][ch];
+      open = rcnt[t] == 1 && rnext[t] == kf;
+    }
+    part[0] = acc;
+  }
+  // the last run starts here and goes on: its later pieces in this chunk added in order; it
+  // is written below if it ends in the chunk (closed), else its piece goes to k_det_join
+  bool closed = false;
+  if (cout && !(nr == 1 && cin)) {
+    float acc = racc[hw][nr - 1][ch];
+    bool open = true;
+    for (int t = hw + 1; open && t < 8; ++t) {
+      acc = acc + racc[t][0][ch];
+      open = rcnt[t] == 1 && rnext[t] == kl;
+    }
+    if (open) {
+      part[(hw == 0 && nr == 1) ? 0 : 32] = acc;  // the chunk's first run (slot 0) or its last
+    } else {
+      racc[hw][nr - 1][ch] = acc;
+      closed = true;
+    }
+  }
+  const bool skip_first = cin, skip_last = cout && !closed;
   const DetRows R = det_rows(m);
   const uint64_t vmask = (uint64_t(1) << d.vbits) - 1;
   // the runs that lie inside the sub-chunk, RG at a time: the group's sparse row ids, then
@@ -242,7 +288,7 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
         const int32_t* rows = j == 0 ? R.rows[0] : j == 1 ? R.rows[1] : R.rows[2];
         float* g = j == 0 ? R.grad[0] : j == 1 ? R.grad[1] : R.grad[2];
         const int64_t rr = rows ? (int64_t)row[u] : (int64_t)((uint64_t)k & vmask);
-        const bool ok = r0 + u < nr && k != invalid && !(r == 0 && prevk == k) && !(r == nr - 1 && nextk == k) &&
+        const bool ok = r0 + u < nr && k != invalid && !(r == 0 && skip_first) && !(r == nr - 1 && skip_last) &&
                         rr >= 0;
         dst[u] = ok ? g + rr * 32 + ch : nullptr;
       }
@@ -251,7 +297,7 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
       for (int u = 0; u < RG; ++u) {
         const int r = r0 + u < nr ? r0 + u : nr - 1;
         const K k = rkey[hw][r];
-        const bool ok = r0 + u < nr && k != invalid && !(r == 0 && prevk == k) && !(r == nr - 1 && nextk == k);
+        const bool ok = r0 + u < nr && k != invalid && !(r == 0 && skip_first) && !(r == nr - 1 && skip_last);
         dst[u] = ok ? det_dst(m, d, (uint64_t)k, ch) : nullptr;
       }
     }
@@ -266,12 +312,12 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
       if (k == invalid) continue;
       const float a = racc[hw][r][ch];
       if (dst[u]) *dst[u] = old[u] + a;
-      else if ((r == 0 && prevk == k) || (r == nr - 1 && nextk == k)) part[r == 0 ? 0 : 32] = a;  // crosses a boundary
     }
   }
 }
 
-// half-wave = sub-chunk s: if a run starts in s and continues past it, sum its pieces.
+// half-wave = chunk s (DCH entries): if a run starts in s and continues past it, sum its
+// pieces.
 // The four neighbour keys are read together and the following sub-chunks' pieces and end
 // keys JOIN_AHEAD at a time (clamped, unconditional loads); the pieces are still added one
 // by one in sub-chunk order
@@ -280,10 +326,10 @@ template <typename K>
 __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int64_t n) {
   const int64_t s = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
   const int ch = threadIdx.x & 31;
-  const int64_t e0 = s * DSUB;
+  const int64_t e0 = s * DCH;
   if (e0 >= n) return;
-  const int64_t e1 = e0 + DSUB < n ? e0 + DSUB : n;
-  const int64_t nsub = (n + DSUB - 1) / DSUB;
+  const int64_t e1 = e0 + DCH < n ? e0 + DCH : n;
+  const int64_t nsub = (n + DCH - 1) / DCH;
   const K* key = reinterpret_cast<const K*>(d.sorted ? d.key[1] : d.key[0]);  // select: a runtime index into the argument copies it to scratch
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
   const K last = key[e1 - 1];
@@ -301,7 +347,7 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
 #pragma unroll
     for (int u = 0; u < JOIN_AHEAD; ++u) {
       const int64_t tt = t + u < nsub ? t + u : nsub - 1;
-      const int64_t te = (tt + 1) * DSUB;
+      const int64_t te = (tt + 1) * DCH;
       pv[u] = d.part[tt * 2 * 32 + ch];
       kv[u] = key[te < n ? te : n - 1];
     }
@@ -310,7 +356,7 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
     for (int u = 0; u < JOIN_AHEAD; ++u) {
       if (!done) {
         acc = acc + pv[u];
-        const int64_t te = (t + u + 1) * DSUB;
+        const int64_t te = (t + u + 1) * DCH;
         done = te >= n || kv[u] != last;  // the run ends inside t + u (or at its end)
       }
     }
@@ -620,10 +666,10 @@ static int det_scatter(const MlpCtx& m, const DetBufs& d0, int64_t n, hipStream_
   if (hipError_t e = hipGetLastError()) return (int)e;
   if (d.temp_bytes < det_sort_temp_bytes(n, d.sort_bits)) return (int)hipErrorInvalidValue;
   if (int e = radix_sort<K>(d, n, d.vbits + 2, s, &d.sorted)) return e;
-  const int64_t nsub = (n + DSUB - 1) / DSUB;
-  hipLaunchKernelGGL(k_det_runs<K>, dim3((unsigned)((nsub + 7) / 8)), dim3(256), 0, s, m, d, n);
+  const int64_t nch = (n + DCH - 1) / DCH;  // chunks = k_det_runs workgroups
+  hipLaunchKernelGGL(k_det_runs<K>, dim3((unsigned)nch), dim3(256), 0, s, m, d, n);
   if (hipError_t e = hipGetLastError()) return (int)e;
-  hipLaunchKernelGGL(k_det_join<K>, dim3((unsigned)((nsub + 7) / 8)), dim3(256), 0, s, m, d, n);
+  hipLaunchKernelGGL(k_det_join<K>, dim3((unsigned)((nch + 7) / 8)), dim3(256), 0, s, m, d, n);
   return (int)hipGetLastError();
 }
 

@@ -87,14 +87,18 @@ struct DetBufs {
   uint64_t* key[2];          // [n_jobs * P * 8] sort keys in / out
   uint32_t* val[2];          // entry ids in / out
   float* w;                  // [n_jobs * P * 8] trilinear weight of each entry
-  float* part;               // [ceil(entries / 32)][2][32] partial sums of the runs that cross a
-                             // 32-entry sub-chunk boundary (k_det_runs -> k_det_join)
+  float* part;               // [ceil(entries / (8 DET_DSUB))][2][32] partial sums of the runs that
+                             // cross a chunk boundary (k_det_runs -> k_det_join)
   void* temp;                // radix-sort scratch: digit counts per tile + digit totals
   size_t temp_bytes;
   int32_t vbits;             // bits of the voxel index; key = job << vbits | voxel
   int32_t sorted;            // which of key[] / val[] holds the sorted entries (set by the sort)
   int32_t sort_bits;         // radix digit width, fixed with the buffers (det_sort_bits)
 };
+#ifndef NC_DET_DSUB
+#define NC_DET_DSUB 16
+#endif
+constexpr int DET_DSUB = NC_DET_DSUB;  // entries per k_det_runs sub-chunk (one half-wave; 8 per chunk)
 int det_sort_bits(int end_bit);
 size_t det_sort_temp_bytes(int64_t n_entries, int bits);
 int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s);
