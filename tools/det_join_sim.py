@@ -1,3 +1,11 @@
+"""CPU check of nc_det.hip's run summation (k_det_runs + k_det_join): a Python model of
+the sub-chunk run sums, the in-chunk join (the half-wave where a run starts adds the later
+pieces in order) and the chunk-level join, run on 400 random run-length patterns (runs of
+1-700 entries, invalid tails) against a plain segmented sum: every voxel written exactly
+once, with its sum.
+
+    python tools/det_join_sim.py
+"""
 import random
 INV = -1
 def simulate(keys, vals, DSUB=16):
