@@ -237,6 +237,7 @@ struct Ws {
   int64_t claim_cap = 0;
   bool claims = false;
   int vbits = 0;
+  int64_t dppad = 0;   // NC_DETERMINISTIC points per job in the entry arrays (det_ppad)
   int dsort_bits = 8;  // NC_DETERMINISTIC radix digit width (det_sort_bits)
   int64_t rec_off[MAX_JOBS] = {0, 0, 0};
   bool save = false;
@@ -357,9 +358,10 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
     w.bslab = take((size_t)pl.n_jobs * w.bslab_rows * DX_BSLAB * 4);
   }
   if (save && vbits > 0) {  // NC_DETERMINISTIC grid-gradient buffers (nc_det.hip)
-    const int64_t ne = (int64_t)pl.n_jobs * P * 8;
+    const int64_t ne = (int64_t)pl.n_jobs * det_ppad(P) * 8;  // each job's points padded to a radix tile
     w.det = true;
     w.vbits = vbits;
+    w.dppad = det_ppad(P);
     w.dfeat = take((size_t)pl.n_jobs * P * 32 * 4);
     for (int b = 0; b < 2; ++b) {
       w.dkey[b] = take((size_t)ne * 8);
@@ -468,6 +470,7 @@ DetBufs det_bufs(void* ws, const Ws& w) {
   d.temp = at<void>(ws, w.dtemp);
   d.temp_bytes = w.dtemp_bytes;
   d.vbits = w.vbits;
+  d.ppad = w.dppad;
   d.sort_bits = w.dsort_bits;
   return d;
 }
@@ -570,7 +573,7 @@ int render_prepare(const nc_render_args* a, Plan& pl, Ws& w, int64_t& P, int& S)
   int vbits = -1;
   if (a->flags & NC_DETERMINISTIC) {
     vbits = stage_vbits(pl, a->grids);
-    if (vbits > 60 || (int64_t)pl.n_jobs * P * 8 >= (int64_t(1) << 32))
+    if (vbits > 60 || (int64_t)pl.n_jobs * det_ppad(P) * 8 >= (int64_t(1) << 32))
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
   layout(a->n_rays, P, pl, true, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, a->loss != NC_LOSS_NONE, w, vbits,
@@ -969,7 +972,7 @@ static int points_prepare(const nc_points_args* a, Plan& pl, Ws& w) {
   int vbits = -1;
   if (a->flags & NC_DETERMINISTIC) {
     vbits = stage_vbits(pl, a->grids);
-    if (vbits > 60 || (int64_t)pl.n_jobs * a->n_points * 8 >= (int64_t(1) << 32))
+    if (vbits > 60 || (int64_t)pl.n_jobs * det_ppad(a->n_points) * 8 >= (int64_t(1) << 32))
       return fail(-1, "nicecore: NC_DETERMINISTIC supports < 2^32 (job, point, corner) entries");
   }
   layout(0, a->n_points, pl, false, (a->flags & NC_SAVE_FOR_BACKWARD) != 0, false, w, vbits,

@@ -4,12 +4,13 @@
 // k_mlp_dx (nc_grid.h), whose summation order varies run to run.  With
 // NC_DETERMINISTIC, k_mlp_dx stores each point's feature gradient instead
 // (MlpCtx::dfeat) and this file reduces them in a fixed order:
-//   k_det_keys    entry (job, point, corner) -> key (job << vbits | voxel), weight
-//   radix sort    a stable LSD radix sort of (key, entry id), 8 bits per pass, written
+//   k_det_keys    entry (job, point, corner) -> key (job << vbits | voxel), weight, and
+//                 the first sort pass's digit counts (one workgroup = one radix tile)
+//   radix sort    a stable LSD radix sort of (key, entry id), 8-11 bits per pass, written
 //                 here (k_rs_hist -> k_rs_scan -> k_rs_scatter): the entries of one voxel
 //                 end up adjacent, in ascending (point, corner) order
 //   k_det_runs /  each voxel run is summed (w * d feature, channel per lane) in
-//   k_det_join    entry order, 32 entries per half-wave, boundary pieces joined in
+//   k_det_join    entry order, 16 entries per half-wave, boundary pieces joined in
 //                 order; one writer per voxel (no atomics)
 // The order is the reference's own: ATen's CPU grid_sampler_3d_backward walks points
 // in order and adds each point's 8 corner contributions (gInp += gOut * w), and a
@@ -46,18 +47,39 @@ __device__ __forceinline__ void store8(T* dst, const T (&v)[8]) {
   }
 }
 
+// radix sort tiles (the sort itself is below, after the run kernels)
+constexpr int RS_THREADS = 256;
+#ifndef NC_RS_ROUNDS
+#define NC_RS_ROUNDS 8  // 2,048-key tiles: 564 workgroups at C2 (16: 282, 5 us slower; 4, 32 slower still)
+#endif
+constexpr int RS_ROUNDS = NC_RS_ROUNDS;
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;
+constexpr int RS_MAX_BITS = 11;
+
+// The first sort pass's digit counts are formed here: a workgroup's 256 points x 8
+// corners are exactly one radix tile (RS_TILE) because each job's points are padded to
+// a multiple of 256 (DetBufs::ppad; the padding entries carry the invalid key), so the
+// tile's row hist[tile][digit] is written here and the pass needs no k_rs_hist.
+constexpr int DET_TILE_POINTS = 256;
+#ifdef NC_DET_NO_KEYS_HIST  // A/B: the first pass counted by k_rs_hist as the others
+constexpr bool KEYS_HIST = false;
+#else
+constexpr bool KEYS_HIST = RS_TILE == 8 * DET_TILE_POINTS;
+#endif
 template <typename K>
-__global__ void __launch_bounds__(256) k_det_keys(const MlpCtx m, DetBufs d) {
+__global__ void __launch_bounds__(DET_TILE_POINTS) k_det_keys(const MlpCtx m, DetBufs d) {
+  __shared__ uint32_t cnt[1 << RS_MAX_BITS];
   K* keys = reinterpret_cast<K*>(d.key[0]);
   const int j = blockIdx.y;
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= m.P) return;
+  const int64_t p = (int64_t)blockIdx.x * DET_TILE_POINTS + threadIdx.x;  // < ppad
+  const int bins = 1 << d.sort_bits;
+  for (int b = threadIdx.x; b < bins; b += DET_TILE_POINTS) cnt[b] = 0u;
   const Job job = job_of(m, j);
   const K invalid = (K)((uint64_t(1) << (d.vbits + 2)) - 1);
-  const int64_t e0 = ((int64_t)j * m.P + p) * 8;
+  const int64_t e0 = ((int64_t)j * d.ppad + p) * 8;
   K kk[8];
   float ww[8];
-  if (!job.need_grid) {
+  if (!job.need_grid || p >= m.P) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       kk[k] = invalid;
@@ -81,6 +103,14 @@ __global__ void __launch_bounds__(256) k_det_keys(const MlpCtx m, DetBufs d) {
   }
   store8(keys + e0, kk);
   store8(d.w + e0, ww);
+  if constexpr (!KEYS_HIST) return;  // (other tile sizes: k_rs_hist counts)
+  __syncthreads();  // counts zeroed
+#pragma unroll
+  for (int k = 0; k < 8; ++k) atomicAdd(&cnt[(int)((uint64_t)kk[k] & (uint64_t)(bins - 1))], 1u);
+  __syncthreads();
+  uint32_t* hist = reinterpret_cast<uint32_t*>(d.temp) +
+                   ((int64_t)j * (d.ppad / DET_TILE_POINTS) + blockIdx.x) * bins;
+  for (int b = threadIdx.x; b < bins; b += DET_TILE_POINTS) hist[b] = cnt[b];
 }
 
 // The sorted entries are cut into sub-chunks of DSUB = 16, one per half-wave (lane =
@@ -185,10 +215,13 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
   const float wraw = d.w[ent];                      // job without a grid gradient: sorted to
   const float myw = myk != invalid ? wraw : 0.f;    // the end) reads row 0 times weight 0 into
                                                     // a run that is never written
-  // every entry's feature-gradient row in flight at once, then weighted
+  // every entry's feature-gradient row in flight at once, then weighted.  Entry id / 8 =
+  // job * ppad + point, the d features are [job][P][32] (no padding): this lane's row
+  const uint32_t q = ent >> 3, jq = (uint32_t)(q >= d.ppad) + (uint32_t)(q >= 2 * d.ppad);
+  const int32_t frow = (int32_t)(q - jq * (uint32_t)(d.ppad - m.P));
   float v[DSUB];
 #pragma unroll
-  for (int i = 0; i < DSUB; ++i) v[i] = m.dfeat[(int64_t)(__shfl(ent, i, 32) >> 3) * 32 + ch];
+  for (int i = 0; i < DSUB; ++i) v[i] = m.dfeat[(int64_t)__shfl(frow, i, 32) * 32 + ch];
 #pragma unroll
   for (int i = 0; i < DSUB; ++i) v[i] = v[i] * __shfl(myw, i, 32);
   int nr = 0;
@@ -400,13 +433,6 @@ __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int
 //                 inside the wave from 8 ballots, wave offsets through LDS; destination =
 //                 exclusive scan of total[] + hist[tile][d] + rank so far
 // ---------------------------------------------------------------------------
-constexpr int RS_THREADS = 256;
-#ifndef NC_RS_ROUNDS
-#define NC_RS_ROUNDS 8  // 2,048-key tiles: 564 workgroups at C2 (16: 282, 5 us slower; 4, 32 slower still)
-#endif
-constexpr int RS_ROUNDS = NC_RS_ROUNDS;
-constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;
-constexpr int RS_MAX_BITS = 11;
 
 template <int BITS, typename K>
 __device__ __forceinline__ int rs_digit(K k, int bit) {
@@ -626,6 +652,7 @@ size_t det_sort_temp_bytes(int64_t n_entries, int bits) {
 
 // sorts key[0] (with the entry ids, taken from the positions by the first pass) by the low
 // end_bit bits; returns the buffer index holding the result
+// (the first pass's counts are k_det_keys' when its workgroups are the sort's tiles)
 template <int BITS, typename K>
 static int radix_sort_w(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, int* sorted) {
   constexpr int BINS = 1 << BITS;
@@ -636,7 +663,8 @@ static int radix_sort_w(const DetBufs& d, int64_t n, int end_bit, hipStream_t s,
   for (int bit = 0; bit < end_bit; bit += BITS) {
     const K* kin = reinterpret_cast<const K*>(d.key[src]);
     K* kout = reinterpret_cast<K*>(d.key[1 - src]);
-    hipLaunchKernelGGL((k_rs_hist<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, n, bit, hist, nt);
+    if (bit > 0 || !KEYS_HIST)
+      hipLaunchKernelGGL((k_rs_hist<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin, n, bit, hist, nt);
     hipLaunchKernelGGL(k_rs_scan<BITS>, dim3(BINS / RS_SCAN_DIG), dim3(RS_THREADS), 0, s, hist, nt, total);
     hipLaunchKernelGGL((k_rs_scatter<BITS, K>), dim3((unsigned)nt), dim3(RS_THREADS), 0, s, kin,
                        bit == 0 ? (const uint32_t*)nullptr : d.val[src], kout,
@@ -662,7 +690,8 @@ static int radix_sort(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, i
 template <typename K>
 static int det_scatter(const MlpCtx& m, const DetBufs& d0, int64_t n, hipStream_t s) {
   DetBufs d = d0;
-  hipLaunchKernelGGL(k_det_keys<K>, dim3((unsigned)((m.P + 255) / 256), m.n_jobs), dim3(256), 0, s, m, d);
+  hipLaunchKernelGGL(k_det_keys<K>, dim3((unsigned)(d.ppad / DET_TILE_POINTS), m.n_jobs), dim3(DET_TILE_POINTS), 0, s,
+                     m, d);
   if (hipError_t e = hipGetLastError()) return (int)e;
   if (d.temp_bytes < det_sort_temp_bytes(n, d.sort_bits)) return (int)hipErrorInvalidValue;
   if (int e = radix_sort<K>(d, n, d.vbits + 2, s, &d.sorted)) return e;
@@ -674,8 +703,9 @@ static int det_scatter(const MlpCtx& m, const DetBufs& d0, int64_t n, hipStream_
 }
 
 int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s) {
-  const int64_t n = (int64_t)m.n_jobs * m.P * 8;
-  if (n == 0) return 0;
+  const int64_t n = (int64_t)m.n_jobs * d.ppad * 8;  // entries, each job's points padded (k_det_keys)
+  if (m.P == 0 || n == 0) return 0;
+  if (d.ppad != det_ppad(m.P)) return (int)hipErrorInvalidValue;
   return d.vbits + 2 <= 32 ? det_scatter<uint32_t>(m, d, n, s) : det_scatter<uint64_t>(m, d, n, s);
 }
 

@@ -84,13 +84,14 @@ struct MlpCtx {
 // accumulation order (ATen's CPU grid_sampler_3d_backward) -- and one owner per voxel
 // sums them in that order.  Run to run bit-identical.
 struct DetBufs {
-  uint64_t* key[2];          // [n_jobs * P * 8] sort keys in / out
+  uint64_t* key[2];          // [n_jobs * ppad * 8] sort keys in / out
   uint32_t* val[2];          // entry ids in / out
-  float* w;                  // [n_jobs * P * 8] trilinear weight of each entry
+  float* w;                  // [n_jobs * ppad * 8] trilinear weight of each entry
   float* part;               // [ceil(entries / (8 DET_DSUB))][2][32] partial sums of the runs that
                              // cross a chunk boundary (k_det_runs -> k_det_join)
   void* temp;                // radix-sort scratch: digit counts per tile + digit totals
   size_t temp_bytes;
+  int64_t ppad;              // points per job in the entry arrays: P rounded up to 256 (det_ppad)
   int32_t vbits;             // bits of the voxel index; key = job << vbits | voxel
   int32_t sorted;            // which of key[] / val[] holds the sorted entries (set by the sort)
   int32_t sort_bits;         // radix digit width, fixed with the buffers (det_sort_bits)
@@ -100,6 +101,7 @@ struct DetBufs {
 #endif
 constexpr int DET_DSUB = NC_DET_DSUB;  // entries per k_det_runs sub-chunk (one half-wave; 8 per chunk)
 int det_sort_bits(int end_bit);
+inline int64_t det_ppad(int64_t P) { return (P + 255) / 256 * 256; }  // one radix tile per 256 points
 size_t det_sort_temp_bytes(int64_t n_entries, int bits);
 int launch_det_scatter(const MlpCtx& m, const DetBufs& d, hipStream_t s);
 

@@ -82,6 +82,7 @@ VARIANTS = {
     "rs_r4": ["-DNC_RS_ROUNDS=4"],
     "rs_r32": ["-DNC_RS_ROUNDS=32"],
     "dsub32": ["-DNC_DET_DSUB=32"],  # NC_DETERMINISTIC=1 runs
+    "det_no_keys_hist": ["-DNC_DET_NO_KEYS_HIST"],
     "det_rg4": ["-DNC_DET_RG=4"],  # NC_DETERMINISTIC=1 runs
     "det_rg16": ["-DNC_DET_RG=16"],
     "no_split": ["-DNC_ABL_NO_SPLIT"],
