@@ -350,10 +350,9 @@ __global__ void __launch_bounds__(256) k_det_runs(const MlpCtx m, DetBufs d, int
 }
 
 // half-wave = chunk s (DCH entries): if a run starts in s and continues past it, sum its
-// pieces.
-// The four neighbour keys are read together and the following sub-chunks' pieces and end
-// keys JOIN_AHEAD at a time (clamped, unconditional loads); the pieces are still added one
-// by one in sub-chunk order
+// pieces.  The four neighbour keys are read together and the following chunks' pieces and
+// end keys JOIN_AHEAD at a time (clamped, unconditional loads); the pieces are still added
+// one by one in chunk order
 constexpr int JOIN_AHEAD = 4;
 template <typename K>
 __global__ void __launch_bounds__(256) k_det_join(const MlpCtx m, DetBufs d, int64_t n) {
