@@ -72,28 +72,34 @@ def simulate(keys, vals, DSUB=16):
         write(last, acc)
     return out
 
-random.seed(1)
-for trial in range(400):
-    n = random.randint(1, 3000)
-    style = trial % 4
-    keys = []
-    k = 0
-    while len(keys) < n:
-        L = random.choice([1, 1, 2, 3, 5, 17, 40, 130, 300, 700]) if style else random.randint(1, 4)
-        keys += [k] * L; k += random.randint(1, 3)
-    keys = keys[:n]
-    if trial % 5 == 0:  # invalid tail
-        m = random.randint(0, n // 3); keys = keys[:n - m] + [10**9] * m
-    keys = [INV if x == 10**9 else x for x in keys]
-    # invalid sorts last: use large sentinel mapped to INV but keep at end
-    vals = [random.random() for _ in range(n)]
-    out = simulate(keys, vals)
-    ref = {}
-    for kk, v in zip(keys, vals):
-        if kk == INV: continue
-        ref[kk] = ref.get(kk, 0.0) + v
-    assert set(out) == set(ref), (trial, set(ref) ^ set(out))
-    for kk in ref:
-        assert out[kk][1] == 1, (trial, kk, out[kk])
-        assert abs(out[kk][0] - ref[kk]) < 1e-9 * max(1, abs(ref[kk])), (trial, kk)
-print("ok")
+def check(trials=400, seed=1):
+    """Random run-length patterns against a plain segmented sum (see the module header)."""
+    random.seed(seed)
+    for trial in range(trials):
+        n = random.randint(1, 3000)
+        style = trial % 4
+        keys = []
+        k = 0
+        while len(keys) < n:
+            L = random.choice([1, 1, 2, 3, 5, 17, 40, 130, 300, 700]) if style else random.randint(1, 4)
+            keys += [k] * L
+            k += random.randint(1, 3)
+        keys = keys[:n]
+        if trial % 5 == 0:  # invalid tail (out-of-grid corners sort last)
+            m = random.randint(0, n // 3)
+            keys = keys[:n - m] + [INV] * m
+        vals = [random.random() for _ in range(n)]
+        out = simulate(keys, vals)
+        ref = {}
+        for kk, v in zip(keys, vals):
+            if kk != INV:
+                ref[kk] = ref.get(kk, 0.0) + v
+        assert set(out) == set(ref), (trial, set(ref) ^ set(out))
+        for kk in ref:
+            assert out[kk][1] == 1, (trial, kk, out[kk])
+            assert abs(out[kk][0] - ref[kk]) < 1e-9 * max(1, abs(ref[kk])), (trial, kk)
+
+
+if __name__ == "__main__":
+    check()
+    print("ok")
