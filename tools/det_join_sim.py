@@ -7,70 +7,92 @@ once, with its sum.
     python tools/det_join_sim.py
 """
 import random
-INV = -1
+
+INV = -1  # the invalid key (out-of-grid corners, padding): sorted last, never written
+
+
 def simulate(keys, vals, DSUB=16):
-    n = len(keys); DCH = 8 * DSUB
-    out = {}  # key -> (value, writes)
+    """keys sorted (INV last), vals per entry -> {key: (sum, number of writes)}."""
+    n = len(keys)
+    DCH = 8 * DSUB
+    out = {}
+
     def write(k, v):
-        c = out.get(k, (0.0, 0)); out[k] = (c[0] + v, c[1] + 1)
+        c = out.get(k, (0.0, 0))
+        out[k] = (c[0] + v, c[1] + 1)
+
     nch = (n + DCH - 1) // DCH
     part = {}
-    for b in range(nch):
+    for b in range(nch):  # k_det_runs: one workgroup per chunk, half-wave hw per sub-chunk
         racc, rkey, rcnt, rnext, info = {}, {}, {}, {}, {}
         for hw in range(8):
-            s = b * 8 + hw; e0 = s * DSUB
+            e0 = (b * 8 + hw) * DSUB
             cnt = 0 if e0 >= n else min(DSUB, n - e0)
             runs = []
             for i in range(cnt):
                 k = keys[e0 + i]
-                if runs and runs[-1][0] == k: runs[-1][1] += vals[e0 + i]
-                else: runs.append([k, vals[e0 + i]])
-            rkey[hw] = [r[0] for r in runs]; racc[hw] = [r[1] for r in runs]; rcnt[hw] = len(runs)
+                if runs and runs[-1][0] == k:
+                    runs[-1][1] += vals[e0 + i]
+                else:
+                    runs.append([k, vals[e0 + i]])
+            rkey[hw] = [r[0] for r in runs]
+            racc[hw] = [r[1] for r in runs]
+            rcnt[hw] = len(runs)
             nextk = keys[e0 + cnt] if (cnt > 0 and e0 + cnt < n) else INV
-            prevk = keys[e0 - 1] if (e0 > 0 and e0 <= n) else INV
+            prevk = keys[e0 - 1] if (0 < e0 <= n) else INV
             rnext[hw] = nextk if cnt > 0 else INV
             info[hw] = (cnt, prevk, nextk)
         for hw in range(8):
             cnt, prevk, nextk = info[hw]
-            if cnt == 0: continue
-            nr = rcnt[hw]; kf = rkey[hw][0]; kl = rkey[hw][nr - 1]
+            if cnt == 0:
+                continue
+            nr = rcnt[hw]
+            kf, kl = rkey[hw][0], rkey[hw][nr - 1]
             cin = kf != INV and prevk == kf
             cout = kl != INV and nextk == kl
-            if hw == 0 and cin:
-                acc = racc[0][0]; open_ = nr == 1 and cout; t = 1
+            if hw == 0 and cin:  # the run continuing from the previous chunk
+                acc, open_, t = racc[0][0], nr == 1 and cout, 1
                 while open_ and t < 8:
-                    acc += racc[t][0]; open_ = rcnt[t] == 1 and rnext[t] == kf; t += 1
+                    acc += racc[t][0]
+                    open_ = rcnt[t] == 1 and rnext[t] == kf
+                    t += 1
                 part[(b, 0)] = acc
             closed = False
-            if cout and not (nr == 1 and cin):
-                acc = racc[hw][nr - 1]; open_ = True; t = hw + 1
+            if cout and not (nr == 1 and cin):  # the last run starts here and goes on
+                acc, open_, t = racc[hw][nr - 1], True, hw + 1
                 while open_ and t < 8:
-                    acc += racc[t][0]; open_ = rcnt[t] == 1 and rnext[t] == kl; t += 1
-                if open_: part[(b, 0 if (hw == 0 and nr == 1) else 1)] = acc
-                else: racc[hw][nr - 1] = acc; closed = True
+                    acc += racc[t][0]
+                    open_ = rcnt[t] == 1 and rnext[t] == kl
+                    t += 1
+                if open_:
+                    part[(b, 0 if (hw == 0 and nr == 1) else 1)] = acc
+                else:
+                    racc[hw][nr - 1] = acc
+                    closed = True
             for r in range(nr):
                 k = rkey[hw][r]
-                if k == INV: continue
-                if r == 0 and cin: continue
-                if r == nr - 1 and cout and not closed: continue
+                if k == INV or (r == 0 and cin) or (r == nr - 1 and cout and not closed):
+                    continue
                 write(k, racc[hw][r])
-    # join
-    for s in range(nch):
-        e0 = s * DCH; e1 = min(e0 + DCH, n)
-        last = keys[e1 - 1]; after = keys[e1] if e1 < n else keys[e1 - 1]
-        first = keys[e0]; before = keys[e0 - 1] if e0 > 0 else keys[e0]
+    for s in range(nch):  # k_det_join: runs crossing chunk boundaries, owned where they start
+        e0, e1 = s * DCH, min(s * DCH + DCH, n)
+        last, first = keys[e1 - 1], keys[e0]
+        after = keys[e1] if e1 < n else keys[e1 - 1]
+        before = keys[e0 - 1] if e0 > 0 else keys[e0]
         cont = last != INV and e1 < n and after == last
         single = first == last
-        if not (cont and not (single and e0 > 0 and before == last)): continue
-        acc = part[(s, 0 if single else 1)]
-        t = s + 1
+        if not (cont and not (single and e0 > 0 and before == last)):
+            continue
+        acc, t = part[(s, 0 if single else 1)], s + 1
         while True:
             acc += part[(t, 0)]
             te = (t + 1) * DCH
-            if te >= n or keys[te] != last: break
+            if te >= n or keys[te] != last:
+                break
             t += 1
         write(last, acc)
     return out
+
 
 def check(trials=400, seed=1):
     """Random run-length patterns against a plain segmented sum (see the module header)."""
