@@ -278,15 +278,11 @@ static bool host_vec_ok(const nc_grid& G) {
 // every grid the stage's decoders look up (the fine decoder: also grid_middle) is
 // channels-last: the forward's trilinear lookups can run inside k_mlp_fwd
 static bool stage_fuse(const Plan& pl, const nc_grid* grids) {
-#ifdef NC_NO_FUSE_GATHER
-  return false;
-#else
   for (int j = 0; j < pl.n_jobs; ++j) {
     const int k = pl.jobs[j].kind;
     if (!host_vec_ok(grids[k]) || (k == K_FINE && !host_vec_ok(grids[K_MID]))) return false;
   }
   return true;
-#endif
 }
 
 void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool loss, Ws& w, int vbits = -1,
@@ -675,9 +671,6 @@ int mlp_backward(const MlpCtx& m, const nc_decoder_params* dec, int64_t P, hipSt
   if (m.bslab && dx_x != m.bslab_rows) return fail(-1, "nicecore: k_mlp_dx grid differs from its workspace rows");
   bool vec = true;  // every grid k_mlp_dx reads is channels-last (device grid_vec_ok)
   for (int j = 0; j < m.n_jobs; ++j) vec = vec && host_vec_ok(m.grids[m.jobs[j].kind]);
-#ifdef NC_DX_NO_VEC  // A/B: the generic (any-stride) k_mlp_dx instantiation
-  vec = false;
-#endif
   if (int e = check_hip(timed(KID_MLP_DX, s, [&] { return launch_mlp_dx(m, dx_x, vec, s); }), "k_mlp_dx")) return e;
   bool any_grid = false;
   for (int j = 0; j < m.n_jobs; ++j) any_grid |= m.jobs[j].need_grid != 0;
@@ -853,11 +846,7 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
   fill_mlp(m, P, pl, a->grids, a->dec, rc.pts, ws, w, false);
   for (int j = 0; j < m.n_jobs; ++j)  // NC_NO_WEIGHT_GRAD: no activation records for k_mlp_dw
     m.jobs[j].keep_h = (a->flags & NC_NO_WEIGHT_GRAD(m.jobs[j].kind)) ? 0 : 1;
-#ifdef NC_ABL_NO_ZERO_FILL  // timing-only ablation: the gradient buffer is not zeroed
-  if (false) {
-#else
   if (a->grad_zero && a->grad_zero_floats > 0) {  // the caller's gradient buffer, zeroed by the gather
-#endif
     if ((reinterpret_cast<uintptr_t>(a->grad_zero) & 15) || (a->grad_zero_floats & 3))
       return fail(-1, "nicecore: grad_zero must be 16-byte aligned and a multiple of 4 floats");
     m.zero_fill = reinterpret_cast<float4*>(a->grad_zero);

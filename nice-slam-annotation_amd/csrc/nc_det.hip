@@ -61,11 +61,7 @@ constexpr int RS_MAX_BITS = 11;
 // a multiple of 256 (DetBufs::ppad; the padding entries carry the invalid key), so the
 // tile's row hist[tile][digit] is written here and the pass needs no k_rs_hist.
 constexpr int DET_TILE_POINTS = 256;
-#ifdef NC_DET_NO_KEYS_HIST  // A/B: the first pass counted by k_rs_hist as the others
-constexpr bool KEYS_HIST = false;
-#else
 constexpr bool KEYS_HIST = RS_TILE == 8 * DET_TILE_POINTS;
-#endif
 template <typename K>
 __global__ void __launch_bounds__(DET_TILE_POINTS) k_det_keys(const MlpCtx m, DetBufs d) {
   __shared__ uint32_t cnt[1 << RS_MAX_BITS];
@@ -689,10 +685,11 @@ static int radix_sort(const DetBufs& d, int64_t n, int end_bit, hipStream_t s, i
 template <typename K>
 static int det_scatter(const MlpCtx& m, const DetBufs& d0, int64_t n, hipStream_t s) {
   DetBufs d = d0;
+  // workspace first: k_det_keys already writes the first pass's tile counts into d.temp
+  if (d.temp_bytes < det_sort_temp_bytes(n, d.sort_bits)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_det_keys<K>, dim3((unsigned)(d.ppad / DET_TILE_POINTS), m.n_jobs), dim3(DET_TILE_POINTS), 0, s,
                      m, d);
   if (hipError_t e = hipGetLastError()) return (int)e;
-  if (d.temp_bytes < det_sort_temp_bytes(n, d.sort_bits)) return (int)hipErrorInvalidValue;
   if (int e = radix_sort<K>(d, n, d.vbits + 2, s, &d.sorted)) return e;
   const int64_t nch = (n + DCH - 1) / DCH;  // chunks = k_det_runs workgroups
   hipLaunchKernelGGL(k_det_runs<K>, dim3((unsigned)nch), dim3(256), 0, s, m, d, n);

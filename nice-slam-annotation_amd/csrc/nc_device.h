@@ -114,7 +114,7 @@ struct Net {
 // ---------------------------------------------------------------------------
 // Split-f16 MFMA ("3 x f16"): every decoder GEMM runs on v_mfma_f32_16x16x32_f16,
 // which issues at 16x the rate of the f32-input MFMA on gfx950.  An f32 operand x
-// is split into hi = f16(x) (round toward zero) and lo = f16((x - hi) * 2^11); a
+// is split into hi = f16(x) and lo = f16((x - hi) * 2^11), both rounded to nearest; a
 // product sum is  sum(a_hi b_hi) + 2^-11 (sum(a_hi b_lo') + sum(a_lo' b_hi))  in two
 // f32 accumulators (the a_lo b_lo term, ~2^-22 relative, is dropped).  Measured on
 // MI355X (tools/split16_bench.hip, profiles/r02/split16_numerics_rate.log): max error
@@ -188,36 +188,12 @@ __host__ __device__ constexpr int hslot(int f) { return 8 * ((f >> 2) & 3) + 4 *
 // hi = RNE(x) leaves r = x - hi exact in f32 (Sterbenz: hi is within a factor 2 of x) with
 // |r| <= half an f16 ulp of x, so lo = RNE(r * 2^11) keeps 11 more bits.
 __device__ __forceinline__ void split8(const float* x, half8& hi, half8& lo) {
-#ifdef NC_ABL_NO_SPLIT  // timing-only ablation: hi only, no lo half (results wrong)
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    const halfx2 h = __builtin_amdgcn_cvt_pkrtz(x[j], x[j + 1]);
-    hi[j] = (_Float16)h[0];
-    hi[j + 1] = (_Float16)h[1];
-    lo[j] = lo[j + 1] = (_Float16)0.f;
-  }
-  return;
-#endif
-#ifdef NC_SPLIT_RTZ  // A/B: the round-4 truncating split
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    const halfx2 h = __builtin_amdgcn_cvt_pkrtz(x[j], x[j + 1]);
-    const float r0 = (x[j] - (float)h[0]) * SPLIT_SCALE;
-    const float r1 = (x[j + 1] - (float)h[1]) * SPLIT_SCALE;
-    const halfx2 l = __builtin_amdgcn_cvt_pkrtz(r0, r1);
-    hi[j] = (_Float16)h[0];
-    hi[j + 1] = (_Float16)h[1];
-    lo[j] = (_Float16)l[0];
-    lo[j + 1] = (_Float16)l[1];
-  }
-#else
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const _Float16 h = (_Float16)x[j];  // v_cvt_f16_f32: round to nearest even
     hi[j] = h;
     lo[j] = (_Float16)((x[j] - (float)h) * SPLIT_SCALE);
   }
-#endif
 }
 
 // the truncating split (round-to-zero halves) the iMAP* layer GEMMs keep: their golden
@@ -242,8 +218,9 @@ __device__ __forceinline__ void split8_rtz(const float* x, half8& hi, half8& lo,
 }
 
 // split8 that also folds max |x| into amax (one v_max_f32 with an |.| modifier per
-// value): the range guard of the split-f16 forward.  hi = f16 RTZ(x) and the residual
-// scaled by 2^11 stay finite and exact-enough only for |x| < 2^15 (RANGE_LIMIT); a tile
+// value): the range guard of the split-f16 forward.  hi = f16(x) (round to nearest even)
+// and the residual scaled by 2^11 stay finite and exact-enough only for |x| < 2^15
+// (RANGE_LIMIT); a tile
 // that saw a larger (or infinite) operand is recomputed on the exact-f32 MFMA path
 // (nc_mlp.hip k_mlp_fwd_exact).  NaN operands pass (fmaxf drops them) and stay NaN, as
 // in the reference's fp32 addmm.
@@ -387,11 +364,6 @@ template <bool VEC>
 __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int g, float out[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) out[j] = 0.f;
-#ifdef NC_ABL_NO_GATHER  // timing-only ablation: no global loads
-#pragma unroll
-  for (int j = 0; j < 8; ++j) out[j] = c.w[j] * 0.01f;
-  return;
-#endif
   const int64_t sC = G.stride[0];
   float v[8][8];
 #pragma unroll
@@ -413,11 +385,7 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
   for (int k = 0; k < 8; ++k) {
     const bool in = VEC || ((c.inb >> k) & 1u);
 #pragma unroll
-#ifdef NC_ABL_NO_TRIW  // timing-only ablation: no weight products (results wrong)
-    for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[k][j] : 0.f);
-#else
     for (int j = 0; j < 8; ++j) out[j] = out[j] + (in ? v[k][j] * c.w[k] : 0.f);
-#endif
   }
 }
 
@@ -426,11 +394,6 @@ __device__ __forceinline__ void gather8(const nc_grid& G, const Corners& c, int 
 // lookup is accumulated exactly as gather8 (bit-identical).
 __device__ __forceinline__ void gather8x2(const nc_grid& G1, const Corners& c1, const nc_grid& G2, const Corners& c2,
                                           int g, float out1[8], float out2[8]) {
-#ifdef NC_ABL_NO_GATHER  // timing-only ablation: no global loads
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { out1[j] = c1.w[j] * 0.01f; out2[j] = c2.w[j] * 0.01f; }
-  return;
-#endif
   float v[2][8][8];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -454,38 +417,7 @@ __device__ __forceinline__ void gather8x2(const nc_grid& G1, const Corners& c1, 
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
 #pragma unroll
-#ifdef NC_ABL_NO_TRIW  // timing-only ablation: no weight products (results wrong)
-      for (int j = 0; j < 8; ++j) out[j] = out[j] + v[q][k][j];
-#else
       for (int j = 0; j < 8; ++j) out[j] = out[j] + v[q][k][j] * c.w[k];  // 0 * w from the zero row
-#endif
-    }
-  }
-}
-
-// gather8 for channels-last grids with half the registers: two batches of 4 corners
-// (offsets from the corner-0 voxel, not Corners::off), same corner order and
-// association, so the result is bit-identical to gather8 / k_grid_gather
-__device__ __forceinline__ void gather8_b2(const nc_grid& G, const Corners& c, int g, float out[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) out[j] = 0.f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float v[4][8];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * h + kk;
-      const float* base = corner_row(G, c, k);  // the zero row for out-of-bounds corners
-      const float4 a = *reinterpret_cast<const float4*>(base + 4 * g);
-      const float4 b = *reinterpret_cast<const float4*>(base + 16 + 4 * g);
-      v[kk][0] = a.x; v[kk][1] = a.y; v[kk][2] = a.z; v[kk][3] = a.w;
-      v[kk][4] = b.x; v[kk][5] = b.y; v[kk][6] = b.z; v[kk][7] = b.w;
-    }
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * h + kk;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) out[j] = out[j] + v[kk][j] * c.w[k];  // 0 * w from the zero row
     }
   }
 }
@@ -501,41 +433,71 @@ __device__ __forceinline__ void normalize_pt(const double p[3], const double (&b
   for (int k = 0; k < 3; ++k) out[k] = (float)(((p[k] - b[k][0]) / (b[k][1] - b[k][0])) * 2.0 - 1.0);
 }
 
-// sin / cos of the Fourier-feature arguments x = p.float() @ B (decoder.py:26-30;
-// |x| reaches ~1e3 rad for room-scale scenes with B ~ N(0, 25^2)).  Cody-Waite
-// reduction of x to [-pi, pi] with a three-part 2*pi, then the hardware
-// v_sin_f32 / v_cos_f32 on the reduced argument in revolutions: 6 VALU instead of
-// ocml's polynomial + Payne-Hanek path.  Measured against float64 over
-// |x| <= 1e3 (tools/sin_accuracy.hip): max abs error 3.8e-7 (ocml sinf 6.8e-8,
-// __sinf 8.8e-5).  The same function is used wherever a feature is recomputed, so
-// forward and backward see identical values.
-__device__ __forceinline__ float reduce_2pi(float x) {
-  const float k = __builtin_rintf(x * 0.15915494309189535f);
-  float r = __builtin_fmaf(-k, 6.28125f, x);
-  r = __builtin_fmaf(-k, 1.9353071795864769e-3f, r);
-  return __builtin_fmaf(-k, 1.2537033403800354e-11f, r);
-}
-// two elements per packed-FP32 instruction (v_pk_mul_f32 / v_pk_fma_f32 on gfx950: each
-// element an IEEE mul / fma, so a packed form is bit-identical to its scalar form)
+// sin / cos of the Fourier-feature arguments x = p.float() @ B (decoder.py:26-30; |x|
+// reaches ~1e3 rad for room-scale scenes with B ~ N(0, 25^2)) to ~1 float32 ulp, as the
+// CPU reference's sinf: Cody-Waite reduction by pi/2 with a three-part constant (c1 =
+// 1.5703125 has 8 significant bits, c2 11: j c1 and j c2 are exact for |j| < 2^15, i.e.
+// |x| < 5e4), the minimax polynomials of sin and cos on [-pi/4, pi/4], and the quadrant
+// j mod 4.  Max error 6.9e-8 over |x| <= 1e3, equal to a correctly rounded float32 sin
+// (tools/sin_accuracy.hip).  Round 6: the former hardware v_sin_f32 after a [-pi, pi]
+// reduction (max error 3.8e-7, 5 float32 ulps of a feature) was the one HIP-specific error
+// of the forward that reaches d raw; the fine_depth golden case's decoder gradients failed
+// the per-element gate on it (tools/diag_chain.py).  Every step is an IEEE
+// mul / fma, so the packed two-argument form is bit-identical to the scalar one (k_mlp_dw
+// recomputes the features with the scalar form).
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-// reduce_2pi of two arguments, returned in revolutions (the argument of v_sin_f32):
-// exactly fourier_sin's reduce_2pi(x) * (1 / 2 pi), element by element
-__device__ __forceinline__ f2 fourier_arg2(f2 x) {
-  const f2 q = x * f2{0.15915494309189535f, 0.15915494309189535f};
-  const f2 k = f2{__builtin_rintf(q.x), __builtin_rintf(q.y)};
-  const f2 nk = -k;
-  f2 r = fma2(nk, f2{6.28125f, 6.28125f}, x);
-  r = fma2(nk, f2{1.9353071795864769e-3f, 1.9353071795864769e-3f}, r);
-  r = fma2(nk, f2{1.2537033403800354e-11f, 1.2537033403800354e-11f}, r);
-  return r * f2{0.15915494309189535f, 0.15915494309189535f};
-}
 
-__device__ __forceinline__ float fourier_sin(float x) {
-  return __builtin_amdgcn_sinf(reduce_2pi(x) * 0.15915494309189535f);
+struct SinCos {
+  float s, c;  // sin, cos of the reduced argument t in [-pi/4, pi/4]
+  int q;       // quadrant: x = t + q pi/2
+};
+constexpr float kTwoOverPi = 0.63661977236758134f;
+constexpr float kPio2_1 = 1.5703125f, kPio2_2 = 4.837512969970703125e-4f, kPio2_3 = 7.5497899548918821e-8f;
+constexpr float kS1 = -1.6666654611e-1f, kS2 = 8.3321608736e-3f, kS3 = -1.9515295891e-4f;
+constexpr float kC1 = 4.166664568298827e-2f, kC2 = -1.388731625493765e-3f, kC3 = 2.443315711809948e-5f;
+
+__device__ __forceinline__ SinCos sincos_reduced(float x) {
+  const float j = __builtin_rintf(x * kTwoOverPi);
+  float t = __builtin_fmaf(-j, kPio2_1, x);
+  t = __builtin_fmaf(-j, kPio2_2, t);
+  t = __builtin_fmaf(-j, kPio2_3, t);
+  const float t2 = t * t;
+  float s = __builtin_fmaf(t2, kS3, kS2);
+  s = __builtin_fmaf(t2, s, kS1);
+  s = __builtin_fmaf(t2 * t, s, t);
+  float c = __builtin_fmaf(t2, kC3, kC2);
+  c = __builtin_fmaf(t2, c, kC1);
+  c = __builtin_fmaf(t2, c, -0.5f);
+  c = __builtin_fmaf(t2, c, 1.0f);
+  return SinCos{s, c, (int)j};
 }
-__device__ __forceinline__ float fourier_cos(float x) {
-  return __builtin_amdgcn_cosf(reduce_2pi(x) * 0.15915494309189535f);
+// sin (shift 0) or cos (shift 1) of x = t + q pi/2
+__device__ __forceinline__ float quadrant_pick(const SinCos& v, int shift) {
+  const int q = (v.q + shift) & 3;
+  const float r = (q & 1) ? v.c : v.s;
+  return (q & 2) ? -r : r;
+}
+__device__ __forceinline__ float fourier_sin(float x) { return quadrant_pick(sincos_reduced(x), 0); }
+__device__ __forceinline__ float fourier_cos(float x) { return quadrant_pick(sincos_reduced(x), 1); }
+
+// fourier_sin of two arguments on packed-FP32 instructions (v_pk_mul / v_pk_fma: IEEE per
+// element), element for element identical to fourier_sin
+__device__ __forceinline__ f2 fourier_sin2(f2 x) {
+  const f2 j = f2{__builtin_rintf(x.x * kTwoOverPi), __builtin_rintf(x.y * kTwoOverPi)};
+  const f2 nj = -j;
+  f2 t = fma2(nj, f2{kPio2_1, kPio2_1}, x);
+  t = fma2(nj, f2{kPio2_2, kPio2_2}, t);
+  t = fma2(nj, f2{kPio2_3, kPio2_3}, t);
+  const f2 t2 = t * t;
+  f2 s = fma2(t2, f2{kS3, kS3}, f2{kS2, kS2});
+  s = fma2(t2, s, f2{kS1, kS1});
+  s = fma2(t2 * t, s, t);
+  f2 c = fma2(t2, f2{kC3, kC3}, f2{kC2, kC2});
+  c = fma2(t2, c, f2{kC1, kC1});
+  c = fma2(t2, c, f2{-0.5f, -0.5f});
+  c = fma2(t2, c, f2{1.0f, 1.0f});
+  return f2{quadrant_pick(SinCos{s.x, c.x, (int)j.x}, 0), quadrant_pick(SinCos{s.y, c.y, (int)j.y}, 0)};
 }
 
 // Sum over the 16 lanes of a DPP row (in the C layout: the 16 points i of one lane-group

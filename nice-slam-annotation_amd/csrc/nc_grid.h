@@ -140,11 +140,7 @@ __device__ __forceinline__ void grid_scatter_flush(const nc_grid& G, const float
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       if (a >= n) break;
-#ifdef NC_ABL_DX_NO_ATOMIC  // timing-only ablation: the walk without its atomics (o is never -7)
-      if (((inb >> k[a]) & 1u) && o[a] == -7) atomicAdd(G.grad + o[a] + chs, v[a]);
-#else
       if (((inb >> k[a]) & 1u) && o[a] >= 0) atomicAdd(G.grad + o[a] + chs, v[a]);
-#endif
     }
   };
   int run = 0;

@@ -309,8 +309,7 @@ constexpr int DX_THREADS = NC_DX_THREADS;   // 12 waves x 16 points, barrier-fre
 #ifndef NC_DW_THREADS
 #define NC_DW_THREADS 1024
 #endif
-// k_mlp_dw: 16 waves own the dW tiles; 16-point sub-chunks (NC_DW_SPLIT16 A/B path: one
-// image-build thread per record row, four per Fourier row, <= 917)
+// k_mlp_dw: 16 waves own the dW tiles; 16-point sub-chunks
 constexpr int DW_THREADS = NC_DW_THREADS;
 
 }  // namespace nc

@@ -31,16 +31,6 @@
 // A/B build: -DNC_MFMA_F32 runs the forward decoder GEMMs on the exact-f32 MFMA
 // (v_mfma_f32_16x16x4_f32, the round-1 kernel) instead of split-f16.
 
-#ifdef NC_ABL_NO_TRIG  // timing-only ablation: no trig at all
-#define NC_SIN(x) (x)
-#define NC_COS(x) (x)
-#define NC_SIN_REV(y) (y)
-#else
-#define NC_SIN fourier_sin
-#define NC_COS fourier_cos
-#define NC_SIN_REV(y) __builtin_amdgcn_sinf(y)  // sin of an argument already in revolutions (fourier_arg2)
-#endif
-
 namespace nc {
 
 // ---------------------------------------------------------------------------
@@ -254,7 +244,6 @@ __device__ __forceinline__ void mac_fwd(const char* M, const char* M3, int kb, c
       mx[t][ob] = mfma16(wl, xh[t], mx[t][ob]);
     }
   }
-#ifndef NC_FWD_W2  // A/B: the round-4 two-plane weights
   // the third planes after both blocks' main products (their fragments not live beside those)
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
@@ -263,7 +252,6 @@ __device__ __forceinline__ void mac_fwd(const char* M, const char* M3, int kb, c
 #pragma unroll
     for (int t = 0; t < T; ++t) mx[t][ob] = mfma16(w3, xh[t], mx[t][ob]);
   }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -305,21 +293,15 @@ __device__ __forceinline__ void mm_fwd_t(const float* W, int qoff, const float* 
                                          floatx4 (&a1)[T], int i, int g) {
   const float* r0 = W + i * LD + 4 * g + 16 * qoff;
   const float* r1 = W + (16 + i) * LD + 4 * g + 16 * qoff;
-#ifdef NC_ABL_FWD_NOLDS  // timing-only ablation: weights never read from LDS
-  float4 w0 = float4{0.01f * i, 0.02f, 0.03f * g, 0.04f}, w1 = float4{0.05f, 0.06f * i, 0.07f, 0.08f * g};
-#else
   float4 w0 = *reinterpret_cast<const float4*>(r0);
   float4 w1 = *reinterpret_cast<const float4*>(r1);
-#endif
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     float4 n0 = w0, n1 = w1;
-#ifndef NC_ABL_FWD_NOLDS
     if (q + 1 < NQ) {
       n0 = *reinterpret_cast<const float4*>(r0 + 16 * (q + 1));
       n1 = *reinterpret_cast<const float4*>(r1 + 16 * (q + 1));
     }
-#endif
     const float wa[4] = {w0.x, w0.y, w0.z, w0.w}, wb[4] = {w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -418,7 +400,7 @@ __device__ __forceinline__ void wave_forward(const float* lds, int i, int g, Wav
       for (int t = 0; t < T; ++t) {
         const float x = __builtin_fmaf(R[t].pf[2], B[2 * EMBP + m],
                                        __builtin_fmaf(R[t].pf[1], B[EMBP + m], R[t].pf[0] * B[m]));
-        R[t].emb[j] = (m < EMB) ? NC_SIN(x) : 0.f;
+        R[t].emb[j] = (m < EMB) ? fourier_sin(x) : 0.f;
       }
     }
   }
@@ -471,10 +453,8 @@ __device__ __forceinline__ void wave_forward(const float* lds, int i, int g, Wav
         const bool p0 = z0[t][r] > 0.f, p1 = z1[t][r] > 0.f;
         hh[r] = p0 ? z0[t][r] : 0.f;
         hh[4 + r] = p1 ? z1[t][r] : 0.f;
-#ifndef NC_ABL_NO_MASK  // timing-only ablation: no relu mask bits
         bits |= (p0 ? 1u : 0u) << r;
         bits |= (p1 ? 1u : 0u) << (4 + r);
-#endif
       }
       if (L < 4) R[t].mask_lo |= bits << (8 * L);
       else R[t].mask_hi = bits;
@@ -572,9 +552,9 @@ __device__ __forceinline__ void wave_forward_h(const char* img, int i, int g, co
           const f2 b1 = *reinterpret_cast<const f2*>(B + EMBP + m);
           const f2 b2 = *reinterpret_cast<const f2*>(B + 2 * EMBP + m);
           const f2 x = fma2(p2, b2, fma2(p1, b1, p0 * b0));
-          const f2 y = fourier_arg2(x);
-          e[j] = NC_SIN_REV(y.x);
-          e[j + 1] = NC_SIN_REV(y.y);
+          const f2 y = fourier_sin2(x);
+          e[j] = y.x;
+          e[j + 1] = y.y;
         }
         split8(e, eh[kb][t], el[kb][t]);
       }
@@ -746,20 +726,6 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
       R[t].pf[0] = nf[t].x; R[t].pf[1] = nf[t].y; R[t].pf[2] = nf[t].z;
       if constexpr (FUSE) {
         const float xyz[3] = {nx[t].x, nx[t].y, nx[t].z};
-#ifdef NC_FWD_GATHER_B2  // A/B: two batches of 4 corners per lookup (fewer registers, more round trips)
-        {
-          const nc_grid& G = ctx.grids[KIND];
-          Corners co;
-          make_corners(G, xyz, co);
-          gather8_b2(G, co, g, R[t].c);
-        }
-        if constexpr (KIND == K_FINE) {  // [fine | middle]: the no-grad grid_middle lookup
-          const nc_grid& G = ctx.grids[K_MID];
-          Corners co;
-          make_corners(G, xyz, co);
-          gather8_b2(G, co, g, R[t].c + 8);
-        }
-#else
         // every corner of the tile's lookups in flight at once (the MLP's registers are
         // free here): one memory round trip per tile
         if constexpr (KIND == K_FINE) {  // [fine | middle]: + the no-grad grid_middle lookup
@@ -775,7 +741,6 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
           make_corners(G, xyz, co);
           gather8<true>(G, co, g, R[t].c);
         }
-#endif
       } else {
 #pragma unroll
         for (int q = 0; q < CQ; ++q) {
@@ -783,11 +748,7 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
           R[t].c[4 * q + 2] = nc[t][q].z; R[t].c[4 * q + 3] = nc[t][q].w;
         }
       }
-#ifdef NC_ABL_NO_RECSTORE  // timing-only ablation: the forward writes no activation record
-      rec[t] = nullptr;
-#else
       rec[t] = (ctx.save_rec && pt[t] < ctx.P) ? ctx.rec + job.rec_off + pt[t] * Rec<KIND>::STRIDE : nullptr;
-#endif
       if constexpr (FUSE) {  // the features k_mlp_dw reads from the record (k_grid_gather's store)
         if (rec[t]) store_rows<CQ>(rec[t] + Rec<KIND>::C, R[t].c, g);
       }
@@ -1029,16 +990,12 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * t + 4 * g + r;
           const float x = __builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m]));
-          dx4[r] = (m < EMB) ? demb[t][r] * NC_COS(x) : 0.f;
+          dx4[r] = (m < EMB) ? demb[t][r] * fourier_cos(x) : 0.f;
           dpf[0] = dpf[0] + B[m] * dx4[r];
           dpf[1] = dpf[1] + B[EMBP + m] * dx4[r];
           dpf[2] = dpf[2] + B[2 * EMBP + m] * dx4[r];
         }
-#ifdef NC_ABL_DX_NO_BGRAD  // timing-only ablation: no Fourier-B weight gradient in dx
-        if (false) {
-#else
         if (need_dw) {  // wave-uniform
-#endif
           *reinterpret_cast<float4*>(slice + i * DXB_LD + 4 * g) = float4{dx4[0], dx4[1], dx4[2], dx4[3]};
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -1079,11 +1036,7 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
         dcv[r] = valid ? dc[0][r] : 0.f;
         dcv[4 + r] = valid ? dc[1][r] : 0.f;
       }
-#ifndef NC_ABL_DX_NO_COORD  // timing-only ablation: no coordinate gradient
       if (need_coord) {
-#else
-      if (false) {
-#endif
         float gi[3] = {0.f, 0.f, 0.f};
         if (JAC) {  // the forward's trilinear Jacobian (NC_SAVE_POINT_JACOBIAN): no corner re-reads
           const float* J = ctx.jac + ((int64_t)job.slot * ctx.P + (valid ? p : 0)) * 96 + 4 * g;
@@ -1115,7 +1068,6 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
           for (int k = 0; k < 3; ++k) dst[k] = gg[k] + (double)dpf[k];
         }
       }
-#ifndef NC_ABL_DX_NO_SCATTER  // timing-only ablation: no grid scatter
       if (need_grid) {
         if (ctx.dfeat) {  // NC_DETERMINISTIC: ordered reduction in nc_det.hip instead of atomics
           if (valid) {
@@ -1127,7 +1079,6 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
           grid_scatter(G, co, dcv, valid, slice, i, g, lane);
         }
       }
-#endif
     }
   }
   if constexpr (N::XYZ) {  // this workgroup's d B partial -> its bslab row (k_mlp_dw folds the rows into its slab)
@@ -1339,13 +1290,10 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
   for (int64_t sub = wg; sub < nsub; sub += nwg) {
     __syncthreads();  // previous sub-chunk's reads are done
     const int64_t p0 = sub * DW_NPTS;
-#ifndef NC_ABL_DW_NO_STAGE  // timing-only ablation: records not copied into LDS
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (dst[k] >= 0) *reinterpret_cast<float4*>(buf + dst[k]) = pre[k];
-#endif
     __syncthreads();
-#ifndef NC_ABL_DW_NO_EMB  // timing-only ablation: no Fourier recompute
     if constexpr (N::XYZ) {  // Fourier features, exactly as wave_forward computes them
       // (rows past P hold p = 0 and padded B columns are 0: sin(0) = 0, no checks)
       const float* B = lds + LY::FB;
@@ -1353,11 +1301,9 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
         const int r = e / EMBP, m = e - r * EMBP;
         const float4 f = *reinterpret_cast<const float4*>(buf + r * LY::RS + LY::PF);
         buf[r * LY::RS + LY::EMB + m] =
-            NC_SIN(__builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m])));
+            fourier_sin(__builtin_fmaf(f.z, B[2 * EMBP + m], __builtin_fmaf(f.y, B[EMBP + m], f.x * B[m])));
       }
     }
-#endif
-#ifndef NC_ABL_DW_NO_MASKPASS  // timing-only ablation: no dZ pass
     // dZ_L = dh_L * relu'(Z_L) (mask bit 8L+j of lane-group g's word; L = 4: hi word)
     for (int e = threadIdx.x; e < DW_NPTS * 40; e += DW_THREADS) {
       const int r = e / 40, c4 = e - r * 40, L = c4 >> 3, jj = c4 & 7;
@@ -1368,11 +1314,8 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
       *reinterpret_cast<float4*>(row + LY::DZ + HID * L + 4 * jj) =
           float4{(w & 1u) ? dh.x : 0.f, (w & 2u) ? dh.y : 0.f, (w & 4u) ? dh.z : 0.f, (w & 8u) ? dh.w : 0.f};
     }
-#endif
     __syncthreads();
-#ifndef NC_ABL_DW_NO_LOAD  // timing-only ablation: the next records are not loaded
     if (sub + nwg < nsub) prefetch(sub + nwg);
-#endif
     if (bcol >= 0) {  // rows past P are zero-filled: they add 0
 #pragma unroll
       for (int r = 0; r < DW_NPTS; ++r) bsum += (double)buf[r * LY::RS + bcol];
@@ -1397,20 +1340,11 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
         }
       }
     };
-#ifdef NC_ABL_DW_NO_MFMA  // timing-only ablation: no k-steps
-    if (false)
-#endif
-    {
-#ifdef NC_DW_PAD_CHAINS  // A/B: every wave runs NS chains (padding slots read zeros)
-      if constexpr (false) {
-#else
-      if constexpr (NS > 1) {
-#endif
-        if (wv + DW_WAVES * (NS - 1) < TL::NT) ksteps(std::integral_constant<int, NS>{});
-        else ksteps(std::integral_constant<int, NS - 1>{});
-      } else {
-        ksteps(std::integral_constant<int, NS>{});
-      }
+    if constexpr (NS > 1) {
+      if (wv + DW_WAVES * (NS - 1) < TL::NT) ksteps(std::integral_constant<int, NS>{});
+      else ksteps(std::integral_constant<int, NS - 1>{});
+    } else {
+      ksteps(std::integral_constant<int, NS>{});
     }
   }
   if (bcol >= 0) bacc[threadIdx.x] = (float)bsum;
@@ -1451,339 +1385,6 @@ __device__ __forceinline__ void dw_job(const MlpCtx& ctx, const Job& job, int j,
 }
 
 
-// ---------------------------------------------------------------------------
-// k_mlp_dw on the split-f16 MFMA (A/B build -DNC_DW_SPLIT16; measured slower than dw_job
-// above: dw 131 vs 92 us at C2, profiles/r04/dw_split16/ -- the per-element split and
-// transpose of the image build costs more than the f32 MFMA k-steps it replaces).
-// dW = sum_points dY^T X with v_mfma_f32_16x16x32_f16, K = 16 points per pair of MFMAs:
-// every operand column (a row of dout / dZ_L / dh_L / h_L / c / the Fourier features
-// of the job) is staged for a 16-point sub-chunk as ONE 64-byte LDS image row
-//   [hi of points 0-7 | hi 8-15 | lo 0-7 | lo 8-15]   (16-B chunks, XOR-swizzled by
-//                                                     (row >> 2) & 3: conflict-free)
-// with x s = hi + lo, s = 2^(14 - exponent(max |x| over the 16 points)) (Fourier rows:
-// |sin| <= 1, s = 2^14): the per-row, per-sub-chunk power-of-two scale puts the row's
-// largest value at 2^14 (no f16 overflow, no subnormal hi); hi = f16(x s), lo = f16(x s
-// - hi) unscaled, so A = [Zh | Zl] (chunks 0-3 by lane group) against B = [Xh | Xh], then
-// [Xl | Xl], gives in two MFMAs  sum_p (Zh + Zl)(Xh + Xl) = s_Y s_X sum_p Z X  (all four
-// products; the split's error ~2^-21 of the row maxima, the f32 MFMA chain's level).
-// The product is unscaled by the exact power of two 1 / (s_Y s_X) into the tile's f32
-// running sum.  Records reach LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
-// wave-instruction: a sub-chunk's 16 contiguous record rows) one sub-chunk ahead,
-// in flight across the image build and the MFMAs; the image build reads them from LDS
-// (one thread per record row, four per Fourier row) -- dZ_L = dh_L relu'(Z_L) from the
-// mask words, the Fourier features recomputed from p.float() with the forward's
-// fourier_sin.  Bias gradients are the dY rows' f32 sums, kept by their threads.
-// ---------------------------------------------------------------------------
-#ifndef NC_DW_RING
-#define NC_DW_RING 2  // record blocks in the split-f16 dW's LDS-DMA ring (3: 135 vs 131 us)
-#endif
-template <int KIND>
-struct DwImg {
-  using N = Net<KIND>;
-  using RC = Rec<KIND>;
-  // image rows
-  static constexpr int ZERO = 0;
-  static constexpr int DOUT0 = 1;
-  static constexpr int DZ0 = DOUT0 + N::NOUT;
-  static constexpr int DH0 = DZ0 + 5 * HID;
-  static constexpr int H0 = DH0 + (N::XYZ ? 5 * HID : 0);  // rows [DOUT0, H0) are dY rows
-  static constexpr int C0 = H0 + 5 * HID;
-  static constexpr int E0 = C0 + N::CD;
-  static constexpr int NROWS = E0 + (N::XYZ ? EMB : 0);
-  static constexpr int NROWSP = (NROWS + 3) & ~3;
-  static constexpr int NREC = E0 - 1;                       // record-sourced rows 1 .. E0 - 1
-  static constexpr int NTHR = NREC + (N::XYZ ? 4 * EMB : 0);  // + four threads per Fourier row
-  static constexpr int RAW = 16 * RC::STRIDE;               // floats of one sub-chunk's records
-  static constexpr int PIECES = (RAW * 4 + 1023) / 1024;    // 1-KiB LDS-DMA pieces
-  static_assert(RAW * 4 == PIECES * 1024, "a sub-chunk's records are whole 1-KiB pieces");
-  // LDS (floats): a ring of NRAW record blocks (the LDS-DMA runs NRAW - 1 sub-chunks ahead)
-  // and one image (the barrier that opens a sub-chunk orders its build after the previous
-  // sub-chunk's MFMA reads)
-  static constexpr int NRAW = NC_DW_RING;
-  static constexpr int RAWB = 0;                          // [NRAW][RAW] record blocks
-  static constexpr int IMG = RAWB + NRAW * RAW;           // [NROWS][16]
-  static constexpr int INV = IMG + NROWS * 16;            // [NROWSP] 1 / s per row
-  static constexpr int FB = INV + NROWSP;                 // [3][EMBP] Fourier B
-  static constexpr int BACC = FB + 3 * EMBP;              // bias accumulators (DwLayout order)
-  static constexpr int TOTAL = BACC + DwLayout<KIND>::BACC_FLOATS;
-  static_assert(NTHR <= DW_THREADS, "one image-build thread per record row, four per Fourier row");
-  // image row of dY row o / X column c of phase ph
-  __device__ static int yrow(int ph, int o) {
-    if (ph == 0) return o < N::NOUT ? DOUT0 + o : ZERO;
-    if (ph <= 5) return DZ0 + HID * (5 - ph) + o;
-    return DH0 + HID * (10 - ph) + o;
-  }
-  __device__ static int xrow(int ph, int c) {
-    if (ph == 0) return H0 + HID * 4 + c;
-    if (ph <= 5) {
-      const int L = 5 - ph;
-      if (L == 0) return N::XYZ ? (c < EMB ? E0 + c : ZERO) : C0 + c;
-      if (L == 3) {
-        if (N::XYZ) return c < EMBP ? (c < EMB ? E0 + c : ZERO) : H0 + HID * 2 + (c - EMBP);
-        return c < HID ? C0 + c : H0 + HID * 2 + (c - HID);
-      }
-      return H0 + HID * (L - 1) + c;
-    }
-    return C0 + c;
-  }
-  // bias-accumulator slot of dY row R (DwLayout's bacc order), -1 for X rows
-  __device__ static int bslot(int R) {
-    if (R < DZ0) return R - DOUT0;
-    if (R < DH0) return 16 + HID * (4 - (R - DZ0) / HID) + (R - DZ0) % HID;             // lin L: ph = 5 - L
-    if (N::XYZ && R < H0) return 16 + HID * (9 - (R - DH0) / HID) + (R - DH0) % HID;  // fc L: ph = 10 - L
-    return -1;
-  }
-};
-
-// byte offset in an image row of 16-B chunk ch (0, 1 hi; 2, 3 lo)
-__device__ __forceinline__ int dw_chunk(int R, int ch) { return R * 64 + 16 * (ch ^ ((R >> 2) & 3)); }
-
-// one LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS byte address
-// lds_dst (wave-uniform) + 16 lane.  Not seen by the compiler's wait counting: the
-// caller retires it with s_waitcnt vmcnt(0) before the barrier that precedes the reads.
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-
-// x s = hi + lo: hi = f16(x s), lo = f16(x s - hi) (x s exact: s a power of two)
-__device__ __forceinline__ _Float16 split_hi(float x, float sc) { return (_Float16)(x * sc); }
-__device__ __forceinline__ _Float16 split_lo(float x, float sc, _Float16 h) { return (_Float16)(x * sc - (float)h); }
-
-template <int KIND>
-__device__ __forceinline__ void dw_job_h(const MlpCtx& ctx, const Job& job, int j, float* lds, int64_t wg,
-                                         int64_t nwg) {
-  using N = Net<KIND>;
-  using RC = Rec<KIND>;
-  using IM = DwImg<KIND>;
-  using TL = DwTiles<KIND>;
-  constexpr int NS = (TL::NT + DW_WAVES - 1) / DW_WAVES;
-  constexpr int NP = 16;  // points per sub-chunk
-  const int t = threadIdx.x, lane = t & 63, i = lane & 15, g = lane >> 4;
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  // ---- roles: record row R = t + 1 (t < NREC); Fourier row E0 + e, points 4q..4q+3 ----
-  const bool rec_row = t < IM::NREC;
-  const bool emb_thr = N::XYZ && !rec_row && t < IM::NTHR;
-  const int R = rec_row ? t + 1 : (emb_thr ? IM::E0 + (t - IM::NREC) / 4 : 0);
-  const int q = (t - IM::NREC) & 3;
-  const bool dz_row = rec_row && R >= IM::DZ0 && R < IM::DH0;
-  int roff = 0, moff = 0, mshift = 0;
-  if (rec_row) {
-    if (R < IM::DZ0) roff = RC::LEN + RC::DOUT + (R - IM::DOUT0);
-    else if (R < IM::DH0) {
-      const int L = (R - IM::DZ0) / HID, f = (R - IM::DZ0) % HID;
-      roff = RC::LEN + RC::DH + HID * L + f;
-      moff = RC::M + 2 * ((f >> 2) & 3) + (L == 4 ? 1 : 0);
-      mshift = (L == 4 ? 0 : 8 * L) + 4 * (f >> 4) + (f & 3);
-    } else if (R < IM::H0) roff = RC::LEN + RC::DH + (R - IM::DH0);
-    else if (R < IM::C0) roff = RC::H + (R - IM::H0);
-    else roff = RC::C + (R - IM::C0);
-  }
-  const int bsl = rec_row ? IM::bslot(R) : -1;
-  float bsum = 0.f;
-  float* bacc = lds + IM::BACC;
-  const int64_t nsub = (ctx.P + NP - 1) / NP;
-  const char* recs = reinterpret_cast<const char*>(ctx.rec + job.rec_off);
-  const uint32_t lds_raw = (uint32_t)reinterpret_cast<uintptr_t>(lds + IM::RAWB);  // LDS byte address
-  // the LDS-DMA of sub-chunk sub into raw block b: wave w issues pieces w and w + 16
-  // (pieces past the block repeat the last one: identical bytes); bytes past the job's
-  // last point read the block's first bytes instead (those points are masked below)
-  auto stage = [&](int64_t sub, int b) {
-#ifdef NC_ABL_DWH_NO_DMA  // timing-only ablation: records not loaded
-    return;
-#endif
-    const int64_t blk = sub * IM::RAW * 4;
-    const int64_t valid = (ctx.P - sub * NP) * (int64_t)RC::STRIDE * 4;
-#pragma unroll
-    for (int k = 0; k < (IM::PIECES + DW_WAVES - 1) / DW_WAVES; ++k) {
-      int pc = wv + DW_WAVES * k;
-      pc = pc < IM::PIECES ? pc : IM::PIECES - 1;
-      const int64_t off = (int64_t)pc * 1024 + 16 * lane;
-      glds16(recs + blk + (off < valid ? off : 0), lds_raw + (uint32_t)(b * IM::RAW * 4 + pc * 1024));
-    }
-  };
-  // ---- prologue: the first NRAW - 1 sub-chunks in flight ----
-#pragma unroll
-  for (int a = 0; a < IM::NRAW - 1; ++a)
-    if (wg + a * nwg < nsub) stage(wg + a * nwg, a);
-  for (int e = t; e < DwLayout<KIND>::BACC_FLOATS; e += blockDim.x) bacc[e] = 0.f;
-  if (t < 4) reinterpret_cast<float4*>(lds + IM::IMG)[t] = float4{0.f, 0.f, 0.f, 0.f};
-  if (t == 0) lds[IM::INV] = 1.f;
-  if constexpr (N::XYZ) {
-    const float* Bsrc = KIND == K_MID ? ctx.dec[K_MID].fourier_B
-                        : KIND == K_FINE ? ctx.dec[K_FINE].fourier_B : ctx.dec[K_COLOR].fourier_B;
-    for (int e = t; e < 3 * EMBP; e += blockDim.x) {
-      const int k = e / EMBP, m = e - k * EMBP;
-      lds[IM::FB + e] = m < EMB ? Bsrc[k * EMB + m] : 0.f;
-    }
-  }
-  // ---- tile descriptors (per lane): image addresses of the A / B chunks, inverse-scale rows ----
-  int ya[NS], xa[NS], yr[NS], xr[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int tau = wv + DW_WAVES * s;
-    int ph, to, ti;
-    TL::get(tau < TL::NT ? tau : 0, ph, to, ti);
-    int yo = IM::yrow(ph, 16 * to + i), xo = IM::xrow(ph, 16 * ti + i);
-    int yi = IM::yrow(ph, 16 * to + 4 * g);
-    if (ph == 0 && 4 * g >= N::NOUT) yi = IM::ZERO;  // rows past NOUT: product 0, any finite scale
-    if (tau >= TL::NT) yo = xo = yi = IM::ZERO;        // padding slot: zero operands, never flushed
-    ya[s] = dw_chunk(yo, g);
-    xa[s] = dw_chunk(xo, g & 1);
-    yr[s] = yi;
-    xr[s] = xo;
-  }
-  floatx4 acc[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) acc[s] = zero4();
-  constexpr int SPW = (IM::PIECES + DW_WAVES - 1) / DW_WAVES;  // LDS-DMA instructions per wave and stage
-  static_assert(IM::NRAW == 2 || IM::NRAW == 3, "ring of 2 or 3 record blocks");
-  int n = 0;
-  for (int64_t sub = wg; sub < nsub; sub += nwg, ++n) {
-    const int b = n % IM::NRAW;
-    // S1: this sub-chunk's records have landed (every wave's pieces; a later sub-chunk's
-    //     stay in flight); the barrier also orders the previous sub-chunk's image reads
-    //     before this build and its raw block's reads before that block's next DMA
-    if (IM::NRAW == 3 && sub + nwg < nsub) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // S2: the sub-chunk NRAW - 1 ahead, in flight across the following iterations
-    if (sub + (IM::NRAW - 1) * nwg < nsub) stage(sub + (IM::NRAW - 1) * nwg, (n + IM::NRAW - 1) % IM::NRAW);
-    // S3: the image from raw block b
-#ifndef NC_ABL_DWH_NO_BUILD  // timing-only ablation: no image build
-    {
-      const float* raw = lds + IM::RAWB + b * IM::RAW;
-      char* img = reinterpret_cast<char*>(lds + IM::IMG);
-      float* inv = lds + IM::INV;
-      const int64_t np = ctx.P - sub * NP;  // valid points in this sub-chunk (>= 1)
-      if (rec_row) {
-        float v[NP];
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          float x = raw[p * RC::STRIDE + roff];
-          if (dz_row) x = ((__float_as_uint(raw[p * RC::STRIDE + moff]) >> mshift) & 1u) ? x : 0.f;
-          v[p] = p < np ? x : 0.f;
-        }
-        if (bsl >= 0) {
-          float s = 0.f;
-#pragma unroll
-          for (int p = 0; p < NP; ++p) s += v[p];
-          bsum += s;
-        }
-        float m = 0.f;
-#pragma unroll
-        for (int p = 0; p < NP; ++p) m = fmaxf(m, fabsf(v[p]));
-        const int e = (int)((__float_as_uint(m) >> 23) & 255u);
-        int sf = (m > 0.f && e < 255) ? 268 - e : 127;  // s = 2^(14 - (e - 127))
-        sf = sf > 254 ? 254 : (sf < 1 ? 1 : sf);
-        const float sc = __uint_as_float((uint32_t)sf << 23);
-        half8 h0, h1, l0, l1;
-#pragma unroll
-        for (int p = 0; p < 8; ++p) {
-          const _Float16 a = split_hi(v[p], sc), c = split_hi(v[p + 8], sc);
-          h0[p] = a;
-          h1[p] = c;
-          l0[p] = split_lo(v[p], sc, a);
-          l1[p] = split_lo(v[p + 8], sc, c);
-        }
-        *reinterpret_cast<half8*>(img + dw_chunk(R, 0)) = h0;
-        *reinterpret_cast<half8*>(img + dw_chunk(R, 1)) = h1;
-        *reinterpret_cast<half8*>(img + dw_chunk(R, 2)) = l0;
-        *reinterpret_cast<half8*>(img + dw_chunk(R, 3)) = l1;
-        inv[R] = __uint_as_float((uint32_t)(254 - sf) << 23);
-      } else if (emb_thr) {
-        const float* B = lds + IM::FB;
-        const int mm = R - IM::E0;
-        const float b0 = B[mm], b1 = B[EMBP + mm], b2 = B[2 * EMBP + mm];
-        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-        half4 h, l;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int p = 4 * q + k;
-          const float4 f = *reinterpret_cast<const float4*>(raw + p * RC::STRIDE + RC::PF);
-          const float x = NC_SIN(__builtin_fmaf(f.z, b2, __builtin_fmaf(f.y, b1, f.x * b0)));
-          const float xv = p < np ? x : 0.f;
-          const _Float16 a = split_hi(xv, 16384.f);  // |sin| <= 1: s = 2^14
-          h[k] = a;
-          l[k] = split_lo(xv, 16384.f, a);
-        }
-        *reinterpret_cast<half4*>(img + dw_chunk(R, q >> 1) + 8 * (q & 1)) = h;
-        *reinterpret_cast<half4*>(img + dw_chunk(R, 2 + (q >> 1)) + 8 * (q & 1)) = l;
-        if (q == 0) inv[R] = 1.f / 16384.f;
-      }
-    }
-#endif
-    // S4: the image is complete (LDS writes retired; the LDS-DMA stays in flight)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // S5: the tiles: two MFMAs per tile over the 16 points, unscaled into the running sums
-    {
-      const char* im = reinterpret_cast<const char*>(lds + IM::IMG);
-      const float* inv = lds + IM::INV;
-      floatx4 P[NS];
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const half8 a = *reinterpret_cast<const half8*>(im + ya[s]);
-        const half8 bh = *reinterpret_cast<const half8*>(im + xa[s]);
-        const half8 bl = *reinterpret_cast<const half8*>(im + (xa[s] ^ 32));
-#ifndef NC_ABL_DWH_NO_MFMA  // timing-only ablation: no MFMAs
-        P[s] = mfma16(a, bh, zero4());
-        P[s] = mfma16(a, bl, P[s]);
-#else
-        P[s] = floatx4{(float)a[0], (float)bh[0], (float)bl[0], 0.f};
-#endif
-      }
-      mfma16_drain();
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const float ix = inv[xr[s]];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[s][r] = __builtin_fmaf(P[s][r], inv[yr[s] + r] * ix, acc[s][r]);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // bias gradients: each dY row's sum, kept by its image-build thread
-  if (bsl >= 0) bacc[bsl] = bsum;
-  // ---- flush (as dw_job): every weight-gradient element owned by one lane ----
-  float* slab = ctx.slab + (int64_t)blockIdx.x * ctx.slab_stride;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int tau = wv + DW_WAVES * s;
-    if (tau >= TL::NT) continue;
-    int ph, to, ti;
-    TL::get(tau, ph, to, ti);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t idx = PhaseMap<KIND>::w_index(ph, 16 * to + 4 * g + r, 16 * ti + i);
-      if (idx >= 0) slab[idx] = acc[s][r];
-    }
-  }
-  __syncthreads();
-  for (int e = t; e < DwLayout<KIND>::BACC_FLOATS; e += blockDim.x) {
-    const int ph = e < 16 ? 0 : 1 + (e - 16) / 32;
-    const int row = e < 16 ? e : (e - 16) % 32;
-    if (ph > 5 && !N::XYZ) continue;
-    const int64_t bi = PhaseMap<KIND>::b_index(ph, row);
-    if (bi >= 0) slab[bi] = bacc[e];
-  }
-  if constexpr (N::XYZ) {  // fourier_B: k_mlp_dx's per-workgroup rows wg, wg + nwg, ... summed in order
-    if (ctx.bslab) {
-      const float* bs = ctx.bslab + (int64_t)j * ctx.bslab_rows * DX_BSLAB;
-      for (int e = t; e < 3 * EMB; e += blockDim.x) {
-        const int c = e / EMB, m = e - c * EMB;
-        float sum = 0.f;
-        for (int64_t r = wg; r < ctx.bslab_rows; r += nwg) sum = sum + bs[r * DX_BSLAB + c * EMBP + m];
-        slab[N::P_B + e] = sum;
-      }
-    }
-  }
-}
-
 __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int b = blockIdx.x;
@@ -1793,17 +1394,10 @@ __global__ void __launch_bounds__(DW_THREADS) k_mlp_dw(const MlpCtx ctx) {
   const int o0 = j == 0 ? ctx.dw_off[0] : (j == 1 ? ctx.dw_off[1] : ctx.dw_off[2]);
   const int o1 = j == 0 ? ctx.dw_off[1] : (j == 1 ? ctx.dw_off[2] : ctx.dw_off[3]);
   switch (job.kind) {
-#ifndef NC_DW_SPLIT16  // the exact-f32 MFMA dW (records staged point-major)
     case K_COARSE: dw_job<K_COARSE>(ctx, job, j, lds, b - o0, o1 - o0); break;
     case K_MID: dw_job<K_MID>(ctx, job, j, lds, b - o0, o1 - o0); break;
     case K_FINE: dw_job<K_FINE>(ctx, job, j, lds, b - o0, o1 - o0); break;
     default: dw_job<K_COLOR>(ctx, job, j, lds, b - o0, o1 - o0); break;
-#else
-    case K_COARSE: dw_job_h<K_COARSE>(ctx, job, j, lds, b - o0, o1 - o0); break;
-    case K_MID: dw_job_h<K_MID>(ctx, job, j, lds, b - o0, o1 - o0); break;
-    case K_FINE: dw_job_h<K_FINE>(ctx, job, j, lds, b - o0, o1 - o0); break;
-    default: dw_job_h<K_COLOR>(ctx, job, j, lds, b - o0, o1 - o0); break;
-#endif
   }
 }
 
@@ -1818,13 +1412,8 @@ constexpr int FWD_LDS_FLOATS =
     FWD_F32 ? FWD_F32_LDS_FLOATS
             : cmax(cmax(NetH<K_COARSE>::BYTES, NetH<K_MID>::BYTES), cmax(NetH<K_FINE>::BYTES, NetH<K_COLOR>::BYTES)) / 4;
 static_assert(FWD_F32_LDS_FLOATS * 4 <= 160 * 1024, "f32 weight image LDS budget");
-#ifndef NC_DW_SPLIT16
 constexpr int DW_LDS_FLOATS = cmax(cmax(DwLayout<K_COARSE>::TOTAL, DwLayout<K_MID>::TOTAL),
                                    cmax(DwLayout<K_FINE>::TOTAL, DwLayout<K_COLOR>::TOTAL));
-#else  // record blocks + split-f16 images + bias accumulators
-constexpr int DW_LDS_FLOATS = cmax(cmax(DwImg<K_COARSE>::TOTAL, DwImg<K_MID>::TOTAL),
-                                   cmax(DwImg<K_FINE>::TOTAL, DwImg<K_COLOR>::TOTAL));
-#endif
 static_assert(FWD_LDS_FLOATS * 4 <= 160 * 1024, "weight image LDS budget");
 static_assert(DW_LDS_FLOATS * 4 <= 160 * 1024, "dW staging LDS budget");
 
@@ -1902,8 +1491,6 @@ int decoder_macs(int kind) {  // SURVEY.md §8a a10-a11 (MAC per point)
 // three xyz decoders, the fine decoder's second feature block a little more
 int fwd_tile_cost(int kind) {
 #if defined(NC_MFMA_F32)
-  return decoder_macs(kind);
-#elif defined(NC_FWD_COST_MACS)
   return decoder_macs(kind);
 #else
   switch (kind) {

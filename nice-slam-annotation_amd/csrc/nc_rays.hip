@@ -166,11 +166,7 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
       z = lower + (upper - lower) * (double)t_rnd;
     }
   }
-#ifdef NC_ABL_NO_SORT  // timing-only ablation: samples left unsorted
-  if (false) {
-#else
   if (c.n_surf > 0 || c.n_extra > 0) {  // Renderer.py:222-224 / :248 torch.sort (bitonic, 64 lanes)
-#endif
 #pragma unroll
     for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll

@@ -226,7 +226,10 @@ def load(path: str | None = None):
         raise NiceCoreError("libnicecore.so ABI version mismatch; rebuild it")
     want = tree_build_id()
     got = lib.nc_build_id().decode()
-    if want is not None and got != want and os.environ.get("NICECORE_ALLOW_STALE") != "1":
+    if want is not None and p != LIB_PATH and "+" in got and got.split("+")[0] == want:
+        import sys  # a variant build of these sources (tools/ablate.py), named explicitly
+        print(f"nicecore: loading variant library {p} (build id {got})", file=sys.stderr, flush=True)
+    elif want is not None and got != want and os.environ.get("NICECORE_ALLOW_STALE") != "1":
         raise NiceCoreError(f"{p} was built from other sources (nc_build_id {got}, this tree {want}); "
                             "rebuild it with `python -m nicecore.build`")
     _lib = lib
@@ -257,7 +260,7 @@ def _ensure_current(p: str):
         import sys
         print(f"nicecore: {p} does not match the sources (build id {B.library_build_id(p)} vs {want}); "
               "rebuilding", file=sys.stderr, flush=True)
-        B.build(force=True)
+        B.build()  # under the build lock: concurrent ranks build once
 
 
 def raw_stream(device) -> int:

@@ -47,8 +47,19 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def variant_suffix(extra=(), arch: str | None = None) -> str:
+    """'' for the product library (gfx950, no extra flags); '+<8 hex>' over the extra
+    compile flags and the target otherwise, so a variant library (tools/ablate.py timing
+    builds, another arch) carries a build id of its own: ``<source hash>+<variant>``."""
+    arch = arch or ARCH
+    if not extra and arch == "gfx950":
+        return ""
+    return "+" + hashlib.sha256((" ".join(extra) + "|" + arch).encode()).hexdigest()[:8]
+
+
 def library_build_id(path: str = LIB) -> str | None:
-    """The source hash embedded in a built library, read from its bytes (no dlopen)."""
+    """The build id embedded in a built library (source hash, plus ``+<variant>`` for a
+    variant build), read from its bytes (no dlopen)."""
     try:
         with open(path, "rb") as fh:
             data = fh.read()
@@ -57,7 +68,8 @@ def library_build_id(path: str = LIB) -> str | None:
     i = data.find(BUILD_ID_TAG)
     if i < 0:
         return None
-    return data[i + len(BUILD_ID_TAG):i + len(BUILD_ID_TAG) + 16].decode("ascii", "replace")
+    j = data.find(b"\0", i)
+    return data[i + len(BUILD_ID_TAG):j if j > 0 else i + len(BUILD_ID_TAG) + 25].decode("ascii", "replace")
 
 
 def have_hipcc() -> bool:
@@ -80,21 +92,42 @@ def needs_build() -> bool:
     return library_build_id(LIB) != source_hash()
 
 
-def build(force: bool = False, verbose: bool = False, extra=(), out: str | None = None) -> str:
+def build(force: bool = False, verbose: bool = False, extra=(), out: str | None = None,
+          csrc: str | None = None, variant: str = "") -> str:
     """Compile libnicecore.so (or, with ``out``, a variant library at that path --
-    timing ablations, tools/ablate.py)."""
+    timing ablations, tools/ablate.py: extra compile flags, or ``csrc`` = a patched copy
+    of the sources, named by ``variant`` in the build id).
+
+    Several processes may call this at once (every rank of a multi-process run loads the
+    library): the build runs under an exclusive lock on ``<lib>.lock``, a process that
+    waited for the lock re-checks the build id before compiling (so N ranks build once),
+    and the link goes to a per-process temporary that is renamed into place atomically
+    (a rank never dlopens a half-written file)."""
+    import fcntl
     lib = out or LIB
     if out is None and not force and not needs_build():
         return LIB
+    with open(lib + ".lock", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        try:
+            if out is None and not force and not needs_build():  # built while we waited
+                return LIB
+            return _build_locked(lib, verbose, extra, csrc or CSRC, variant)
+        finally:
+            fcntl.flock(lock, fcntl.LOCK_UN)
+
+
+def _build_locked(lib: str, verbose: bool, extra, csrc: str, variant: str) -> str:
+    vid = variant_suffix([*extra, variant] if variant else extra)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
-             "-Wno-unused-function", "-Wno-unused-variable", "-I", INCLUDE, "-I", CSRC,
-             f'-DNC_SRC_HASH="{source_hash()}"', *extra]
+             "-Wno-unused-function", "-Wno-unused-variable", "-I", INCLUDE, "-I", csrc,
+             f'-DNC_SRC_HASH="{source_hash()}{vid}"', *extra]
     # one hipcc per source in parallel, then one link: the wall time is the slowest file
     with tempfile.TemporaryDirectory(prefix="nicecore_build_") as tmp:
         objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
 
         def compile_one(k):
-            cmd = [hipcc(), *flags, "-c", "-o", objs[k], os.path.join(CSRC, SOURCES[k])]
+            cmd = [hipcc(), *flags, "-c", "-o", objs[k], os.path.join(csrc, SOURCES[k])]
             if verbose:
                 print(" ".join(cmd), flush=True)
             return subprocess.run(cmd, capture_output=True, text=True)
@@ -107,11 +140,12 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str | None 
                 raise RuntimeError(f"hipcc failed on {src}:\n" + r.stdout + r.stderr)
             if verbose and (r.stdout or r.stderr):
                 print(r.stdout + r.stderr)
-        r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp", *objs],
+        tmp_lib = f"{lib}.{os.getpid()}.tmp"
+        r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp_lib, *objs],
                            capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("hipcc link failed:\n" + r.stdout + r.stderr)
-    os.replace(lib + ".tmp", lib)
+    os.replace(tmp_lib, lib)
     return lib
 
 

@@ -79,6 +79,33 @@ def run_case(name, device="cuda", channels_last=False, want=("rays", "grids", "p
     return rec, {k: v.detach().cpu() for k, v in got.items()}
 
 
+def hip_render_grads(grids, params, bound, cbound, ro, rd, stage, gt, upstream, channels_last=True,
+                     make=None):
+    """The HIP render + backward of given inputs (the drop-in Renderer, grids on the GPU in
+    the chosen layout), upstream gradients ``upstream`` = (d depth, d var, d color); returns
+    {name: cpu tensor} like run_case."""
+    model = build_model(params, bound, cbound, "cuda")
+    g = {}
+    for k, v in grids.items():
+        t = v.cuda()
+        if channels_last:
+            t = t.contiguous(memory_format=torch.channels_last_3d)
+        g[k] = t.requires_grad_(True)
+    ro_g, rd_g = ro.cuda().requires_grad_(True), rd.cuda().requires_grad_(True)
+    r = (make or make_renderer)(bound)
+    d, v, c = r.render_batch_ray(g, model, rd_g, ro_g, "cuda", stage, gt.cuda() if gt is not None else None)
+    torch.autograd.backward([d, v, c], [t.cuda() for t in upstream])
+    got = {"depth": d.detach(), "var": v.detach(), "color": c.detach(), "grad/rays_o": ro_g.grad,
+           "grad/rays_d": rd_g.grad}
+    for k, t in g.items():
+        if t.grad is not None:
+            got["grad/" + k] = t.grad
+    for n, p in model.named_parameters():
+        if p.grad is not None:
+            got["grad/param/" + n] = p.grad
+    return {k: t.detach().cpu() for k, t in got.items()}
+
+
 def rel_err(got, ref):
     """max |got - ref| / max(|ref|_max, tiny) — scale-aware error of a whole tensor."""
     got = got.double().reshape(-1)
@@ -321,6 +348,33 @@ def oracle_mapper_refs(w, kw, stage="color", forms=((False, False, None), (True,
     return refs
 
 
+# --- C1 (BASELINE configs[0]) golden cases: tests/golden/make_golden_c1.py ---------------
+C1_CASES = [
+    # name, middle-grid scale, middle occupancy bias (None: the initialiser's), upstream seed
+    ("c1_room0", 1.0, None, 71),
+    ("c1_room0_spread", 30.0, -0.55, 72),
+]
+
+
+def c1_inputs(name):
+    """(scene, grids, params, rays (ro, rd)) of a C1 golden case, regenerated from the seeds
+    the generator used (init_grids seed 0 as bench.build_workload, build_default_nice seed
+    0 = the reference's get_model under torch.manual_seed(0), synth_rays seed 1000)."""
+    from nicecore import decoder as D
+    from nicecore import scene as S
+    scale, bias = next((s, b) for n, s, b, _ in C1_CASES if n == name)
+    sc = S.make_scene("replica_room0")
+    grids = S.init_grids(sc.shapes, generator=torch.Generator().manual_seed(0))
+    grids = {k: (v * scale if k == "grid_middle" else v).contiguous() for k, v in grids.items()}
+    m = D.build_default_nice(seed=0)
+    if bias is not None:
+        with torch.no_grad():
+            m.middle_decoder.output_linear.bias.fill_(bias)
+    params = {k: v.detach().clone() for k, v in m.named_parameters()}
+    ro, rd, _, _ = S.synth_rays(sc, 200, seed=1000)
+    return sc, grids, params, (ro, rd)
+
+
 def c2_args(**over):
     """bench.py's default C2 arguments (Replica room0, 1000 rays, stage color, BA)."""
     import types
@@ -405,7 +459,25 @@ def permuted_problem(grids, params, seed):
     return new_g, new_p, unpermute
 
 
-def oracle_render_grads_permuted(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, seed):
+def oracle_render_grads_permuted(grids, params, dec_b, bound, ro, rd, stage, gt, upstream, seed, depth_max=None):
     """oracle_render_grads (float32) of the unit-permuted network, in the original order."""
     g2, p2, un = permuted_problem(grids, params, seed)
-    return un(oracle_render_grads(g2, p2, dec_b, bound, ro, rd, stage, gt, upstream))
+    return un(oracle_render_grads(g2, p2, dec_b, bound, ro, rd, stage, gt, upstream, depth_max=depth_max))
+
+
+def oracle_elementwise_gate(title, got, grids, params, dec_b, bound, ro, rd, stage, gt, upstream, depth_max=None):
+    """The per-element gate (elementwise_vs_truth) of a HIP result ``got`` on any inputs:
+    truth = the float64 oracle with the reference's float32 input roundings, refs = the
+    float32 oracle and two unit-permuted float32 oracles; prints the table and returns the
+    failing tensors, plus any gradient HIP produces that the reference does not (must be
+    zero), under "extra"."""
+    args = (grids, params, dec_b, bound, ro, rd, stage, gt, upstream)
+    truth = oracle_render_grads(*args, f64=True, round_inputs=True, depth_max=depth_max)
+    ref32 = oracle_render_grads(*args, depth_max=depth_max)
+    refs = [ref32] + [oracle_render_grads_permuted(*args, seed=s, depth_max=depth_max) for s in (1, 2)]
+    truth = {k: v for k, v in truth.items() if k in ref32}
+    bad = report_elementwise(title, elementwise_vs_truth(got, refs, truth))
+    extra = [k for k in got if k.startswith("grad/") and k not in ref32 and float(got[k].abs().max()) > 0]
+    if extra:
+        bad["extra"] = extra
+    return bad

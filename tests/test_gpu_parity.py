@@ -130,12 +130,12 @@ def _room0_case(n_rays, stage, seed=7):
 @pytest.mark.gpu
 @pytest.mark.parametrize("stage", ["color", "middle"])
 def test_room0_against_oracle(stage):
-    """Benchmark geometry (Replica room0 bound and grid shapes), 256 rays.  Scored
-    against a float64 ground truth: the HIP error must stay within 4x the fp32
-    reference's own error (floors 2e-5 outputs / 2e-4 gradients) -- gradient
-    reductions over thousands of points cancel, so a plain relative bound is the
-    wrong metric there."""
-    from parity_common import oracle_render_grads, score_vs_truth
+    """Benchmark geometry (Replica room0 bound and grid shapes), 256 rays, channels-last
+    grids, under the per-element gate (parity_common.oracle_elementwise_gate: every
+    element within 4x the largest float32 oracle error against the float64 truth plus 4x
+    the float32 RMS error, grid-gradient support, no extra gradients).  The reference's
+    own vectors at this geometry: tests/test_gpu_elementwise.py::test_c1_golden_elementwise."""
+    from parity_common import hip_render_grads, oracle_elementwise_gate
     sc, grids, params, ro, rd, dep = _room0_case(256, stage)
     cb = sc.bound * 2
     dec_b = {"coarse": cb, "middle": sc.bound, "fine": sc.bound, "color": sc.bound}
@@ -144,27 +144,9 @@ def test_room0_against_oracle(stage):
     gd = torch.randn(ro.shape[0], generator=gen, dtype=torch.float64)
     gv = torch.randn(ro.shape[0], generator=gen, dtype=torch.float64)
     gc = torch.randn(ro.shape[0], 3, generator=gen)
-    ref32 = oracle_render_grads(grids, params, dec_b, sc.bound, ro, rd, stage, gt, (gd, gv, gc))
-    ref64 = oracle_render_grads(grids, params, dec_b, sc.bound, ro, rd, stage, gt, (gd, gv, gc), f64=True)
-    # HIP (channels-last grids, the fast layout)
-    model = build_model(params, sc.bound, cb, "cuda")
-    ro_g, rd_g = ro.cuda().requires_grad_(True), rd.cuda().requires_grad_(True)
-    g_g = {k: v.cuda().contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
-           for k, v in grids.items()}
-    r = make_renderer(sc.bound)
-    d_g, v_g, c_g = r.render_batch_ray(g_g, model, rd_g, ro_g, "cuda", stage,
-                                       gt.cuda() if gt is not None else None)
-    torch.autograd.backward([d_g, v_g, c_g], [gd.cuda(), gv.cuda(), gc.cuda()])
-    got = {"depth": d_g.detach().cpu(), "var": v_g.detach().cpu(), "color": c_g.detach().cpu(),
-           "grad/rays_o": ro_g.grad.cpu(), "grad/rays_d": rd_g.grad.cpu()}
-    for k, v in g_g.items():
-        if v.grad is not None:
-            got["grad/" + k] = v.grad.cpu()
-    for n, p in model.named_parameters():
-        if p.grad is not None:
-            got["grad/param/" + n] = p.grad.cpu()
-    scores = score_vs_truth(got, ref32, ref64)
-    bad = {k: v for k, v in scores.items() if not v[0] <= v[2]}
+    got = hip_render_grads(grids, params, sc.bound, cb, ro, rd, stage, gt, (gd, gv, gc))
+    bad = oracle_elementwise_gate(f"room0 256 rays {stage}", got, grids, params, dec_b, sc.bound, ro, rd, stage, gt,
+                                  (gd, gv, gc))
     assert not bad, bad
 
 

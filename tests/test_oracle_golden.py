@@ -61,6 +61,42 @@ def test_oracle_sample_points_and_raw(case):
     torch.testing.assert_close(raw, rec["raw"], rtol=0, atol=0)
 
 
+# ---- C1 = BASELINE configs[0] (tests/golden/make_golden_c1.py) ----
+from parity_common import C1_CASES, c1_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("case", [c[0] for c in C1_CASES])
+def test_oracle_c1_golden(case):
+    """Replica room0, 200 rays x 32 samples, stage middle: the oracle (float32, the
+    reference's op order) on the regenerated grids / parameters against the reference's
+    own outputs and gradients at BASELINE's configs[0]."""
+    sc, grids, params, (ro0, rd0) = c1_inputs(case)
+    rec = load_case(case)
+    assert torch.equal(ro0, rec["rays_o"]) and torch.equal(rd0, rec["rays_d"])  # same rays regenerated
+    ro = rec["rays_o"].clone().requires_grad_(True)
+    rd = rec["rays_d"].clone().requires_grad_(True)
+    g = {k: v.clone().requires_grad_(True) for k, v in grids.items()}
+    prm = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    dec_bounds = {"coarse": sc.bound * 2, "middle": sc.bound, "fine": sc.bound, "color": sc.bound}
+    depth, var, color = O.render_batch_ray(g, prm, dec_bounds, sc.bound, rd, ro, "middle", None)
+    torch.autograd.backward([depth, var, color], [rec["g_depth"], rec["g_var"], rec["g_color"]])
+    torch.testing.assert_close(depth.detach(), rec["depth"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(var.detach(), rec["var"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(color.detach(), rec["color"], rtol=0, atol=0)
+    torch.testing.assert_close(ro.grad, rec["grad/rays_o"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rd.grad, rec["grad/rays_d"], rtol=1e-5, atol=1e-6)
+    gm = rec["grad/grid_middle"]
+    torch.testing.assert_close(g["grid_middle"].grad, gm, rtol=1e-5, atol=1e-6 * float(gm.abs().max()))
+    for k in ("grid_coarse", "grid_fine", "grid_color"):
+        assert g[k].grad is None or float(g[k].grad.abs().max()) == 0.0
+    for k, v in prm.items():
+        key = "grad/param/" + k
+        if key in rec:
+            torch.testing.assert_close(v.grad, rec[key], rtol=1e-5, atol=1e-6 * float(rec[key].abs().max()))
+        else:
+            assert v.grad is None or float(v.grad.abs().max()) == 0.0
+
+
 # ---- iMAP* (tests/golden/make_golden_imap.py) ----
 import json  # noqa: E402
 import os  # noqa: E402
