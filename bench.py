@@ -485,8 +485,22 @@ def cpu_baseline(args, seconds):
         if el >= seconds or n >= 50:
             break
     return {"value": args.rays * n / el, "unit": "rays/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{n} iterations x {args.rays} rays x {samples_per_ray(args)} samples, stage {args.stage}, "
                       f"{args.mode} grads, torch CPU fp32/fp64 oracle, {threads} threads"}
+
+
+def cpu_model() -> str:
+    """The host CPU's model name (report the core count and CPU model)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
 
 
 def read_traffic(args):

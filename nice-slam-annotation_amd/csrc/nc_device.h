@@ -434,70 +434,73 @@ __device__ __forceinline__ void normalize_pt(const double p[3], const double (&b
 }
 
 // sin / cos of the Fourier-feature arguments x = p.float() @ B (decoder.py:26-30; |x|
-// reaches ~1e3 rad for room-scale scenes with B ~ N(0, 25^2)) to ~1 float32 ulp, as the
-// CPU reference's sinf: Cody-Waite reduction by pi/2 with a three-part constant (c1 =
-// 1.5703125 has 8 significant bits, c2 11: j c1 and j c2 are exact for |j| < 2^15, i.e.
-// |x| < 5e4), the minimax polynomials of sin and cos on [-pi/4, pi/4], and the quadrant
-// j mod 4.  Max error 6.9e-8 over |x| <= 1e3, equal to a correctly rounded float32 sin
-// (tools/sin_accuracy.hip).  Round 6: the former hardware v_sin_f32 after a [-pi, pi]
-// reduction (max error 3.8e-7, 5 float32 ulps of a feature) was the one HIP-specific error
-// of the forward that reaches d raw; the fine_depth golden case's decoder gradients failed
-// the per-element gate on it (tools/diag_chain.py).  Every step is an IEEE
-// mul / fma, so the packed two-argument form is bit-identical to the scalar one (k_mlp_dw
-// recomputes the features with the scalar form).
+// reaches ~1e3 rad for room-scale scenes with B ~ N(0, 25^2)) to about one float32 ulp, as
+// the CPU reference's sinf: x = t + k pi with k = rint(x / pi) (the 1.5 2^23 magic-number
+// round, exact for |x| < 2^22 pi, whose low mantissa bit is k's parity), t by Cody-Waite with
+// a three-part pi (pi1 = 3.140625 has 8 significant bits: k pi1 is exact for |k| < 2^16),
+// then sin t = t + t^3 P(t^2) / cos t = 1 + t^2 Q(t^2) (minimax on [-pi/2, pi/2], fitted
+// by tools/sin_fit.py) and the sign (-1)^k.  Over |x| <= 1.2e3 (tools/sin_fit.py float32
+// emulation): sin max error 1.23e-7, mean 1.55e-8 (a correctly rounded float32 sin: 6.9e-8,
+// 1.32e-8); cos 1.41e-7, 2.2e-8.  Round 6: the former hardware v_sin_f32 after a [-pi, pi]
+// reduction (max error 3.8e-7, 5 float32 ulps of a feature) was the one HIP-specific error of
+// the forward that reaches d raw; the fine_depth golden case's decoder gradients failed the
+// per-element gate on it (tools/diag_chain.py).  Every step is an IEEE mul /
+// fma / add or an integer op, so the packed two-argument form (v_pk_fma_f32) is bit-identical
+// to the scalar one (k_mlp_dw recomputes the features with the scalar form); the packed
+// form issues 15 instructions per pair of features against the v_sin form's 7 plus two
+// quarter-rate transcendentals.
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-struct SinCos {
-  float s, c;  // sin, cos of the reduced argument t in [-pi/4, pi/4]
-  int q;       // quadrant: x = t + q pi/2
-};
-constexpr float kTwoOverPi = 0.63661977236758134f;
-constexpr float kPio2_1 = 1.5703125f, kPio2_2 = 4.837512969970703125e-4f, kPio2_3 = 7.5497899548918821e-8f;
-constexpr float kS1 = -1.6666654611e-1f, kS2 = 8.3321608736e-3f, kS3 = -1.9515295891e-4f;
-constexpr float kC1 = 4.166664568298827e-2f, kC2 = -1.388731625493765e-3f, kC3 = 2.443315711809948e-5f;
+constexpr float kInvPi = 0.318309886183790672f;
+constexpr float kRoundMagic = 12582912.f;  // 1.5 * 2^23
+constexpr float kPi1 = 3.140625f, kPi2 = 9.676535897930e-4f, kPi3 = 5.126566e-12f;
+constexpr float kS1 = -0.16666657f, kS2 = 0.008333017f, kS3 = -0.00019806615f, kS4 = 2.6000544e-06f;
+constexpr float kC1 = -0.5f, kC2 = 0.04166664f, kC3 = -0.0013888404f, kC4 = 2.4761886e-05f, kC5 = -2.6077103e-07f;
 
-__device__ __forceinline__ SinCos sincos_reduced(float x) {
-  const float j = __builtin_rintf(x * kTwoOverPi);
-  float t = __builtin_fmaf(-j, kPio2_1, x);
-  t = __builtin_fmaf(-j, kPio2_2, t);
-  t = __builtin_fmaf(-j, kPio2_3, t);
+// t = x - k pi and (-1)^k as a sign bit
+__device__ __forceinline__ float reduce_pi(float x, unsigned& sign) {
+  const float y = __builtin_fmaf(x, kInvPi, kRoundMagic);
+  const float k = y - kRoundMagic;
+  sign = __float_as_uint(y) << 31;
+  float t = __builtin_fmaf(-k, kPi1, x);
+  t = __builtin_fmaf(-k, kPi2, t);
+  return __builtin_fmaf(-k, kPi3, t);
+}
+__device__ __forceinline__ float fourier_sin(float x) {
+  unsigned sg;
+  const float t = reduce_pi(x, sg);
   const float t2 = t * t;
-  float s = __builtin_fmaf(t2, kS3, kS2);
-  s = __builtin_fmaf(t2, s, kS1);
-  s = __builtin_fmaf(t2 * t, s, t);
-  float c = __builtin_fmaf(t2, kC3, kC2);
-  c = __builtin_fmaf(t2, c, kC1);
-  c = __builtin_fmaf(t2, c, -0.5f);
-  c = __builtin_fmaf(t2, c, 1.0f);
-  return SinCos{s, c, (int)j};
+  float p = __builtin_fmaf(t2, kS4, kS3);
+  p = __builtin_fmaf(t2, p, kS2);
+  p = __builtin_fmaf(t2, p, kS1);
+  return __uint_as_float(__float_as_uint(__builtin_fmaf(t2 * t, p, t)) ^ sg);
 }
-// sin (shift 0) or cos (shift 1) of x = t + q pi/2
-__device__ __forceinline__ float quadrant_pick(const SinCos& v, int shift) {
-  const int q = (v.q + shift) & 3;
-  const float r = (q & 1) ? v.c : v.s;
-  return (q & 2) ? -r : r;
+__device__ __forceinline__ float fourier_cos(float x) {
+  unsigned sg;
+  const float t = reduce_pi(x, sg);
+  const float t2 = t * t;
+  float p = __builtin_fmaf(t2, kC5, kC4);
+  p = __builtin_fmaf(t2, p, kC3);
+  p = __builtin_fmaf(t2, p, kC2);
+  p = __builtin_fmaf(t2, p, kC1);
+  return __uint_as_float(__float_as_uint(__builtin_fmaf(t2, p, 1.f)) ^ sg);
 }
-__device__ __forceinline__ float fourier_sin(float x) { return quadrant_pick(sincos_reduced(x), 0); }
-__device__ __forceinline__ float fourier_cos(float x) { return quadrant_pick(sincos_reduced(x), 1); }
 
-// fourier_sin of two arguments on packed-FP32 instructions (v_pk_mul / v_pk_fma: IEEE per
-// element), element for element identical to fourier_sin
+// fourier_sin of two arguments on packed-FP32 instructions, element for element identical
 __device__ __forceinline__ f2 fourier_sin2(f2 x) {
-  const f2 j = f2{__builtin_rintf(x.x * kTwoOverPi), __builtin_rintf(x.y * kTwoOverPi)};
-  const f2 nj = -j;
-  f2 t = fma2(nj, f2{kPio2_1, kPio2_1}, x);
-  t = fma2(nj, f2{kPio2_2, kPio2_2}, t);
-  t = fma2(nj, f2{kPio2_3, kPio2_3}, t);
+  const f2 y = fma2(x, f2{kInvPi, kInvPi}, f2{kRoundMagic, kRoundMagic});
+  const f2 nk = f2{kRoundMagic, kRoundMagic} - y;  // -k (exact)
+  f2 t = fma2(nk, f2{kPi1, kPi1}, x);
+  t = fma2(nk, f2{kPi2, kPi2}, t);
+  t = fma2(nk, f2{kPi3, kPi3}, t);
   const f2 t2 = t * t;
-  f2 s = fma2(t2, f2{kS3, kS3}, f2{kS2, kS2});
-  s = fma2(t2, s, f2{kS1, kS1});
-  s = fma2(t2 * t, s, t);
-  f2 c = fma2(t2, f2{kC3, kC3}, f2{kC2, kC2});
-  c = fma2(t2, c, f2{kC1, kC1});
-  c = fma2(t2, c, f2{-0.5f, -0.5f});
-  c = fma2(t2, c, f2{1.0f, 1.0f});
-  return f2{quadrant_pick(SinCos{s.x, c.x, (int)j.x}, 0), quadrant_pick(SinCos{s.y, c.y, (int)j.y}, 0)};
+  f2 p = fma2(t2, f2{kS4, kS4}, f2{kS3, kS3});
+  p = fma2(t2, p, f2{kS2, kS2});
+  p = fma2(t2, p, f2{kS1, kS1});
+  const f2 s = fma2(t2 * t, p, t);
+  return f2{__uint_as_float(__float_as_uint(s.x) ^ (__float_as_uint(y.x) << 31)),
+            __uint_as_float(__float_as_uint(s.y) ^ (__float_as_uint(y.y) << 31))};
 }
 
 // Sum over the 16 lanes of a DPP row (in the C layout: the 16 points i of one lane-group

@@ -34,7 +34,9 @@ __device__ __forceinline__ void quad_terms(const T (&q)[4], T (&P)[3][3]) {
 }
 
 // c2w rows 0..2 of frame f: the caller's matrix, or get_camera_from_tensor(cam[f])
-// (common.py:163-176: [quad2rotation(q) | t])
+// (common.py:163-176: [quad2rotation(q) | t]).  quad2rotation writes R into a float32
+// tensor (common.py:150) whatever the quaternion's dtype: R is rounded to float (a no-op
+// for T = float), t keeps T.
 template <typename T>
 __device__ __forceinline__ void pose_rows(const nc_sample_args& a, int64_t f, T (&M)[3][4]) {
   if (a.cam) {
@@ -47,7 +49,7 @@ __device__ __forceinline__ void pose_rows(const nc_sample_args& a, int64_t f, T 
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) M[r][c] = r == c ? (T)1 - s * P[r][c] : s * P[r][c];
+      for (int c = 0; c < 3; ++c) M[r][c] = (T)(float)(r == c ? (T)1 - s * P[r][c] : s * P[r][c]);
       M[r][3] = cam_at<T>(a, f, 4 + r);
     }
   } else {
@@ -60,7 +62,8 @@ __device__ __forceinline__ void pose_rows(const nc_sample_args& a, int64_t f, T 
 }
 
 // d loss / d cam from d loss / d c2w (G: 3 x 4): the chain rule through quad2rotation --
-// dR_ab/dq_m = sigma_ab (ds/dq_m P_ab + s dP_ab/dq_m), ds/dq_m = -s 2 q_m / |q|^2
+// dR_ab/dq_m = sigma_ab (ds/dq_m P_ab + s dP_ab/dq_m), ds/dq_m = -s 2 q_m / |q|^2.  The
+// rotation's gradient passes the reference's float32 rot_mat: rounded to float first.
 template <typename T>
 __device__ __forceinline__ void cam_grad(const T (&q)[4], const T (&G)[12], T (&gc)[7]) {
   const T n = ((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3];
@@ -79,7 +82,8 @@ __device__ __forceinline__ void cam_grad(const T (&q)[4], const T (&G)[12], T (&
   for (int r = 0; r < 3; ++r)
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const T sg = r == c ? -G[r * 4 + c] : G[r * 4 + c];
+      const T gr = (T)(float)G[r * 4 + c];
+      const T sg = r == c ? -gr : gr;
       gsP += sg * P[r][c];
 #pragma unroll
       for (int m = 0; m < 4; ++m) gdP[m] += sg * dP[r][c][m];

@@ -70,18 +70,23 @@ def frames(H0, H1, W0, W1, indices, fx, fy, cx, cy, c2ws, depths, colors, bound=
 def quad2rotation(quad):
     """common.py:137-160 for a batch [B, 4] of quaternions (qr, qi, qj, qk): the rotation with
     two_s = 2 / |q|^2 (a quaternion off unit norm, as Adam leaves it, still maps to a
-    rotation-like matrix the same way as the reference's)."""
+    rotation-like matrix the same way as the reference's).  The reference assigns the
+    entries into ``torch.zeros(bs, 3, 3)`` (float32, common.py:150), so R is rounded to
+    float32 whatever the quaternion's dtype, and its gradient passes that float32 tensor
+    (rounded to float32) on the way back; get_camera_from_tensor's torch.cat then promotes
+    R to the translation's dtype (common.py:173)."""
     qr, qi, qj, qk = quad[:, 0], quad[:, 1], quad[:, 2], quad[:, 3]
     two_s = 2.0 / (quad * quad).sum(-1)
     rows = [[1 - two_s * (qj ** 2 + qk ** 2), two_s * (qi * qj - qk * qr), two_s * (qi * qk + qj * qr)],
             [two_s * (qi * qj + qk * qr), 1 - two_s * (qi ** 2 + qk ** 2), two_s * (qj * qk - qi * qr)],
             [two_s * (qi * qk - qj * qr), two_s * (qj * qk + qi * qr), 1 - two_s * (qi ** 2 + qj ** 2)]]
-    return torch.stack([torch.stack(r, -1) for r in rows], -2)
+    R = torch.stack([torch.stack(r, -1) for r in rows], -2)
+    return R.float()
 
 
 def camera_from_tensor(inputs):
     """common.py:163-176 get_camera_from_tensor: [B, 7] (or [7]) -> [B, 3, 4] (or [3, 4])."""
     one = inputs.dim() == 1
     x = inputs.unsqueeze(0) if one else inputs
-    RT = torch.cat([quad2rotation(x[:, :4]), x[:, 4:, None]], 2)
+    RT = torch.cat([quad2rotation(x[:, :4]).to(x.dtype), x[:, 4:, None]], 2)
     return RT[0] if one else RT

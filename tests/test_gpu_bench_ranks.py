@@ -92,3 +92,20 @@ def test_gloo_ranks_apartment_frustum_rows(tmp_path):
     assert line["n_gpus"] == 2 and line["config"]["rays_per_gpu"] == 625
     assert line["config"]["grid_exchange"].startswith("frustum rows")
     _check_equal(one, two, 2, 1250)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gloo_ranks_c4_apartment_world8(tmp_path):
+    """BASELINE C4 as stated: Apartment, one 5,000-ray window (40 keyframes x 125 rays,
+    synth_rays' 40 poses), 8 ranks of 625 rays (gloo, on this one GPU), the frustum-row
+    exchange with the grid all-reduce beside k_mlp_dw (overlap on): the rank-summed
+    frustum-row and decoder gradients equal one rank's 5,000-ray step to 1e-5 of max-abs."""
+    one_line, one = _one_rank(tmp_path, "apartment", 5000)
+    line, eight = _bench(tmp_path, "apartment_w8", "--gpus", "8", "--backend", "gloo", "--scene", "apartment",
+                         "--global-rays", "5000", "--overlap", "on")
+    assert line["n_gpus"] == 8 and line["config"]["rays_per_gpu"] == 625
+    assert line["config"]["parallelism"] == "dp8"
+    assert line["config"]["grid_exchange"].startswith("frustum rows")
+    assert line["config"]["overlap"] == "grid all-reduce beside k_mlp_dw"
+    _check_equal(one, eight, 8, 5000)

@@ -199,3 +199,25 @@ def test_hip_camera_tensor_sampling(dtype):
                                                      indices=idx[:1])
     (rd3.sum() + ro3.sum()).backward()
     assert c3.grad.shape == (7,) and bool(torch.isfinite(c3.grad).all())
+
+
+def test_oracle_camera_tensor_rotation_is_float32():
+    """common.py:150: quad2rotation assigns R into torch.zeros(bs, 3, 3) -- float32 whatever
+    the quaternion's dtype -- and get_camera_from_tensor's cat promotes it (common.py:173):
+    a float64 camera tensor gives float32-rounded rotation entries and a float64
+    translation, and R's gradient is rounded to float32 on its way to the quaternion."""
+    gen = torch.Generator().manual_seed(3)
+    cam = torch.cat([torch.randn(2, 4, generator=gen, dtype=torch.float64),
+                     torch.randn(2, 3, generator=gen, dtype=torch.float64)], 1).requires_grad_(True)
+    RT = SO.camera_from_tensor(cam)
+    assert RT.dtype == torch.float64
+    R = RT[:, :, :3].detach()
+    assert torch.equal(R, R.float().double())  # float32-representable
+    assert torch.equal(RT[:, :, 3].detach(), cam[:, 4:].detach())  # translation untouched
+    g = torch.randn(RT.shape, generator=gen, dtype=torch.float64)
+    (RT * g).sum().backward()
+    # the same chain with the upstream rotation gradient rounded to float32 by hand
+    q = cam.detach()[:, :4].clone().requires_grad_(True)
+    R64 = SO.quad2rotation(q)
+    (R64.double() * g[:, :, :3].float().double()).sum().backward()
+    assert torch.equal(cam.grad[:, :4], q.grad)

@@ -23,6 +23,16 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "nice-slam-annotation_amd"))
 DBG = os.path.join(REPO, "dbg")
 
+_VSREV = """__device__ __forceinline__ float _vs_rev(float x) {  // round-5 reduce_2pi, in revolutions
+  const float k = __builtin_rintf(x * 0.15915494309189535f);
+  float r = __builtin_fmaf(-k, 6.28125f, x);
+  r = __builtin_fmaf(-k, 1.9353071795864769e-3f, r);
+  r = __builtin_fmaf(-k, 1.2537033403800354e-11f, r);
+  return r * 0.15915494309189535f;
+}
+"""
+_VSIN2 = "  return f2{__builtin_amdgcn_sinf(_vs_rev(x.x)), __builtin_amdgcn_sinf(_vs_rev(x.y))};\n"
+
 # (file, anchor, replacement): the anchor must occur exactly once in the file
 PATCHES = {
     "no_gather": [
@@ -59,6 +69,15 @@ PATCHES = {
     ],
     "no_sort": [
         ("nc_rays.hip", "  if (c.n_surf > 0 || c.n_extra > 0) {  // Renderer.py:222-224", "  if (false) {  // Renderer.py:222-224"),
+    ],
+    "vsin": [  # the round-5 Fourier sin / cos: [-pi, pi] Cody-Waite + hardware v_sin_f32 / v_cos_f32
+        ("nc_device.h", "__device__ __forceinline__ f2 fourier_sin2(f2 x) {\n",
+         "__device__ __forceinline__ f2 fourier_sin2(f2 x) {\n" + _VSIN2),
+        ("nc_device.h", "__device__ __forceinline__ float fourier_sin(float x) {\n",
+         "__device__ __forceinline__ float fourier_sin(float x) {\n  return __builtin_amdgcn_sinf(_vs_rev(x));\n"),
+        ("nc_device.h", "__device__ __forceinline__ float fourier_cos(float x) {\n",
+         "__device__ __forceinline__ float fourier_cos(float x) {\n  return __builtin_amdgcn_cosf(_vs_rev(x));\n"),
+        ("nc_device.h", "// t = x - k pi and (-1)^k as a sign bit\n", _VSREV + "// t = x - k pi and (-1)^k as a sign bit\n"),
     ],
     "no_zero_fill": [
         ("nc_abi.hip", "  if (a->grad_zero && a->grad_zero_floats > 0) {", "  if (false) {"),
@@ -130,11 +149,14 @@ def build_variant(name):
 
 
 def run_variant(name):
-    lib = os.path.join(DBG, f"abl_{name}.so")
-    if not os.path.exists(lib):
-        print(name, "missing", flush=True)
-        return True
-    env = dict(os.environ, NICECORE_LIB=lib)
+    """``cur``: the in-tree product library; any other name: dbg/abl_<name>.so."""
+    env = dict(os.environ)
+    if name != "cur":
+        lib = os.path.join(DBG, f"abl_{name}.so")
+        if not os.path.exists(lib):
+            print(name, "missing", flush=True)
+            return True
+        env["NICECORE_LIB"] = lib
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "3",
                         "--cpu-seconds", "0"], env=env, capture_output=True, text=True, timeout=300)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
