@@ -476,7 +476,18 @@ __device__ __forceinline__ float fourier_sin(float x) {
   p = __builtin_fmaf(t2, p, kS1);
   return __uint_as_float(__float_as_uint(__builtin_fmaf(t2 * t, p, t)) ^ sg);
 }
+// cos x for the Fourier backward (k_mlp_dx: d (p @ B) = d emb * cos(p @ B)): Cody-Waite by
+// 2 pi and the hardware v_cos_f32 (3.8e-7 max error).  It reaches only the point and
+// Fourier-B gradients, per point; the polynomial form (fourier_cos_poly, 1.4e-7) cost
+// k_mlp_dx 10 us at C2 (120.7 vs 110.8, same box, profiles/r06/sin/) and is kept for reference.
 __device__ __forceinline__ float fourier_cos(float x) {
+  const float k = __builtin_rintf(x * 0.15915494309189535f);
+  float r = __builtin_fmaf(-k, 6.28125f, x);
+  r = __builtin_fmaf(-k, 1.9353071795864769e-3f, r);
+  r = __builtin_fmaf(-k, 1.2537033403800354e-11f, r);
+  return __builtin_amdgcn_cosf(r * 0.15915494309189535f);
+}
+__device__ __forceinline__ float fourier_cos_poly(float x) {
   unsigned sg;
   const float t = reduce_pi(x, sg);
   const float t2 = t * t;

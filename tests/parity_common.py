@@ -408,10 +408,11 @@ def permuted_problem(grids, params, seed):
         pre = d + "_decoder."
         xyz = d != "coarse"
         pi = [rp(32) for _ in range(5)]
+        ident = torch.arange(32)  # a decoder whose grid is not in the problem (C5 windows: no coarse grid)
         if d == "fine":
-            cin = torch.cat([rho["grid_fine"], 32 + rho["grid_middle"]])
+            cin = torch.cat([rho.get("grid_fine", ident), 32 + rho.get("grid_middle", ident)])
         else:
-            cin = rho[_DECODER_GRID[d]]
+            cin = rho.get(_DECODER_GRID[d], ident)
         sig = rp(93) if xyz else None
         for L in range(5):
             if L == 0:

@@ -157,6 +157,7 @@ def run_variant(name):
             print(name, "missing", flush=True)
             return True
         env["NICECORE_LIB"] = lib
+        env["NICECORE_ALLOW_STALE"] = "1"  # a variant may be built from another revision (A/B)
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "3",
                         "--cpu-seconds", "0"], env=env, capture_output=True, text=True, timeout=300)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
