@@ -974,6 +974,7 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
       const float* B = lds + N::FB;
       const float4 f = valid ? ctx.pf[p] : float4{0.f, 0.f, 0.f, 0.f};
       constexpr int DXB_LD = 24;  // [point][16 features] rows: 16-B aligned, 2 lanes per bank on the reads
+      static_assert(16 * DXB_LD <= SCAT_FLOATS, "the d B staging fits the wave's scatter slice");
       float pfa[4];  // A operand of k-step s: p.float()[i] of point 4 s + g (lane i < 3)
       if (need_dw) {
 #pragma unroll

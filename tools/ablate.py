@@ -90,6 +90,7 @@ DEFINES = {
     "ref": [],
     "mfma_f32": ["-DNC_MFMA_F32"],  # the exact-f32 MFMA forward (a numerics A/B, results valid)
     "dx512": ["-DNC_DX_THREADS=512"],
+    "dx1024": ["-DNC_DX_THREADS=1024"],  # 16 waves: 4 per SIMD at <= 128 VGPRs
     "dw512_16": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=16"],
     "dw256_16": ["-DNC_DW_THREADS=256", "-DNC_DW_NPTS=16"],
     "dw1024_16": ["-DNC_DW_THREADS=1024", "-DNC_DW_NPTS=16"],
