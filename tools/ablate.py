@@ -79,6 +79,9 @@ PATCHES = {
          "__device__ __forceinline__ float fourier_cos(float x) {\n  return __builtin_amdgcn_cosf(_vs_rev(x));\n"),
         ("nc_device.h", "// t = x - k pi and (-1)^k as a sign bit\n", _VSREV + "// t = x - k pi and (-1)^k as a sign bit\n"),
     ],
+    "swz3_old": [  # the round-5 third-plane swizzle (2-way LDS bank conflicts on its reads; results valid)
+        ("nc_device.h", "return 16 * (g ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3));", "return 16 * (g ^ ((row >> 2) & 3));"),
+    ],
     "no_zero_fill": [
         ("nc_abi.hip", "  if (a->grad_zero && a->grad_zero_floats > 0) {", "  if (false) {"),
     ],

@@ -44,3 +44,6 @@ for k, c in sorted(vals.items()):
           f"busy per mfma {busy / max(mf, 1):.1f} cyc")
     print(f"   lds_bank_conflict/active_lds {g('SQ_LDS_BANK_CONFLICT') / max(g('SQ_ACTIVE_INST_LDS'), 1):.3f}  "
           f"active_valu/wave_cycles {g('SQ_ACTIVE_INST_VALU') / wc:.2f}")
+    if g('SQ_LDS_IDX_ACTIVE') > 0:
+        print(f"   lds_bank_conflict {g('SQ_LDS_BANK_CONFLICT'):.3e} of lds_idx_active {g('SQ_LDS_IDX_ACTIVE'):.3e} "
+              f"({g('SQ_LDS_BANK_CONFLICT') / g('SQ_LDS_IDX_ACTIVE'):.3f})")

@@ -13,11 +13,12 @@ mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 C1="SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_F16 SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
 C2="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_WAVES"
+C3="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES"
 for v in "${vars[@]}"; do
   lib="$ROOT/dbg/abl_$v.so"
   [ -f "$lib" ] || { echo "missing $lib"; exit 2; }
   n=0
-  for C in "$C1" "$C2"; do
+  for C in "$C1" "$C2" "$C3"; do
     n=$((n+1))
     echo "=== $v pass $n"
     NICECORE_LIB="$lib" timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "$krx" --output-format csv \
