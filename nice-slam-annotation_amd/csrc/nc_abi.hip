@@ -17,6 +17,7 @@
 
 #include "nc_device.h"
 #include "nc_internal.h"
+#include "nc_wimage.h"
 
 using namespace nc;
 
@@ -224,7 +225,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, rflag = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
+  size_t dmax = 0, rflag = 0, wimg = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
          gocc_b = 0, grgb_b = 0,  // fused mapper loss: d raw of a backward that is not d loss alone
          lpart = 0, lcount = 0,   // fused mapper loss: per-workgroup partial sums + done counter
          coef_d = 0, coef_c = 0, bslab = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
@@ -295,6 +296,7 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
   };
   w.dmax = take(16);
   w.rflag = take(4 * MAX_JOBS);  // MlpCtx::range_flag
+  w.wimg = take((size_t)pl.n_jobs * WIMG_STRIDE);  // MlpCtx::wimg (nc_wimage.h)
   w.z = rays ? take((size_t)P * 8) : 0;
   w.pts = rays ? take((size_t)P * 24) : 0;
   w.xyz = take((size_t)pl.n_jobs * P * 16);
@@ -450,9 +452,23 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   }
   m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
   m.range_flag = at<uint32_t>(ws, w.rflag);
+  m.wimg = at<char>(ws, w.wimg);
   m.bslab = w.save ? at<float>(ws, w.bslab) : nullptr;
   m.bslab_rows = w.bslab_rows;
   m.jac = w.has_jac ? at<float>(ws, w.jac) : nullptr;
+}
+
+// the weight-image builders of k_ray_setup / k_points_prep for k_mlp_fwd's jobs (nc_wimage.h)
+static WImgCtx wimg_ctx(const MlpCtx& m) {
+  WImgCtx wi;
+  std::memset(&wi, 0, sizeof(wi));
+  wi.n_jobs = m.n_jobs;
+  wi.img = const_cast<char*>(m.wimg);
+  for (int j = 0; j < m.n_jobs; ++j) {
+    wi.kind[j] = m.jobs[j].kind;
+    wi.dec[j] = m.dec[m.jobs[j].kind];
+  }
+  return wi;
 }
 
 DetBufs det_bufs(void* ws, const Ws& w) {
@@ -870,7 +886,7 @@ int nc_render_forward(const nc_render_args* a, void* ws, size_t ws_bytes, void* 
     m.zero_fill = nullptr;
     m.zero_n4 = 0;
   }
-  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
+  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, wimg_ctx(m), s); }), "k_ray_setup")) return e;
   if (int e = gather_and_claim(m, w, s)) return e;
   if (!m.fuse_gather) {  // zeroed by k_grid_gather (else by k_mlp_fwd)
     m.zero_fill = nullptr;
@@ -988,7 +1004,7 @@ int nc_points_forward(const nc_points_args* a, void* ws, size_t ws_bytes, void* 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   MlpCtx m;
   fill_mlp(m, a->n_points, pl, a->grids, a->dec, a->pts, ws, w, false);
-  if (int e = check_hip(launch_points_prep(m, (float4*)m.xyz, (float4*)m.pf, s), "k_points_prep")) return e;
+  if (int e = check_hip(launch_points_prep(m, wimg_ctx(m), (float4*)m.xyz, (float4*)m.pf, s), "k_points_prep")) return e;
   if (int e = gather_and_claim(m, w, s)) return e;
   if (int e = check_hip(timed(KID_MLP_FWD, s, [&] { return launch_mlp_fwd(m, s); }), "k_mlp_fwd")) return e;
   return check_hip(timed(KID_POINTS_ASSEMBLE, s, [&] { return launch_points_assemble(m, a->stage, a->raw, s); }), "k_points_assemble");
@@ -1497,7 +1513,9 @@ int nc_imap_render_forward(const nc_imap_render_args* a, void* ws, size_t ws_byt
       return e;
     }
   }
-  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, s); }), "k_ray_setup")) return e;
+  WImgCtx no_img;  // iMAP*: no NICE decoder images
+  std::memset(&no_img, 0, sizeof(no_img));
+  if (int e = check_hip(timed(KID_RAY_SETUP, s, [&] { return launch_ray_setup(rc, no_img, s); }), "k_ray_setup")) return e;
   float* raw = at<float>(ws, w.raw);
   if (int e = imap_mlp_forward(a->dec, P, ws, w, raw, s)) return e;
   if (int e = check_hip(launch_imap_split(raw, P, at<float>(ws, w.occ), at<float>(ws, w.rgb), s), "k_imap_split"))

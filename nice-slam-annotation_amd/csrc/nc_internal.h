@@ -28,6 +28,15 @@ constexpr int MAX_JOBS = 3;
 constexpr int CLAIM_SHARDS = 64;
 static_assert(CLAIM_SHARDS <= 64, "k_rows_compact sums the shard counters across one wavefront");
 
+// Split-f16 forward weight images (nc_wimage.h): extra workgroups of the kernel before
+// k_mlp_fwd (k_ray_setup, k_points_prep) build job j's image at img + j * WIMG_STRIDE.
+struct WImgCtx {
+  int32_t n_jobs;      // 0: no builder workgroups
+  int32_t kind[MAX_JOBS];
+  char* img;           // [n_jobs][WIMG_STRIDE] (MlpCtx::wimg)
+  nc_decoder_params dec[MAX_JOBS];
+};
+
 // Arguments of the point-batched decoder kernels.
 struct MlpCtx {
   int64_t P;                 // number of points
@@ -73,6 +82,8 @@ struct MlpCtx {
   int32_t bslab_rows;        // k_mlp_dx workgroup (= its grid x); k_mlp_dw moves them into its slab
   const double* dout_scale;  // device scalar multiplying gocc / grgb in k_mlp_dx (d loss of a fused
                              // mapper loss, RayCtx::fuse_bwd), or NULL
+  const char* wimg;          // [n_jobs][WIMG_STRIDE] split-f16 weight images + flag words (nc_wimage.h),
+                             // built by the kernel before k_mlp_fwd (WImgCtx)
   uint32_t* range_flag;      // [MAX_JOBS] split-f16 range guard: k_mlp_fwd sets job j's word when
                              // an operand reached RANGE_LIMIT, k_mlp_fwd_exact then recomputes the
                              // job in f32; zeroed by k_ray_setup / k_points_prep (NULL: no guard)
@@ -259,7 +270,7 @@ constexpr int DX_BSLAB = 3 * 96;  // floats per k_mlp_dx workgroup: d B [3][EMBP
 
 // kernels: launch wrappers (return hipError_t as int)
 int launch_depth_max(const float* gt, const uint8_t* valid, int64_t n, float* out, hipStream_t s);
-int launch_ray_setup(const RayCtx& c, hipStream_t s);
+int launch_ray_setup(const RayCtx& c, const WImgCtx& wi, hipStream_t s);
 int launch_composite_fwd(const RayCtx& c, hipStream_t s);
 int launch_composite_fwd_loss(const RayCtx& c, hipStream_t s);
 int launch_composite_bwd(const RayCtx& c, hipStream_t s);
@@ -271,7 +282,7 @@ int launch_points_assemble(const MlpCtx& m, int stage, float* raw, hipStream_t s
 int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, float* gocc, float* grgb,
                              hipStream_t s);
 int launch_points_grads(const MlpCtx& m, double* g_pts, hipStream_t s);
-int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s);
+int launch_points_prep(const MlpCtx& m, const WImgCtx& wi, float4* xyz, float4* pf, hipStream_t s);
 
 int mlp_fwd_lds_bytes();
 int mlp_dw_lds_bytes();

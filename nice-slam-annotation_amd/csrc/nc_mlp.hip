@@ -27,6 +27,7 @@
 #include "nc_device.h"
 #include "nc_grid.h"
 #include "nc_internal.h"
+#include "nc_wimage.h"
 
 // A/B build: -DNC_MFMA_F32 runs the forward decoder GEMMs on the exact-f32 MFMA
 // (v_mfma_f32_16x16x4_f32, the round-1 kernel) instead of split-f16.
@@ -129,98 +130,19 @@ __device__ __forceinline__ void load_weights(float* lds, const nc_decoder_params
   __syncthreads();
 }
 
-// Split-f16 forward weight image (NetH, nc_device.h).  Same one-round-trip prologue as
-// load_weights: all global loads, zero-fill, barrier, hi/lo half stores, barrier.
-template <int KIND>
-__device__ __forceinline__ int hpos(int m, int o, int c, int plane) {  // byte offset of W_m[o][packed c]
-  using H = NetH<KIND>;
-  const int row = (c >> 5) * 32 + o;
-  const int s = hslot(c & 31);
-  if (plane == 2) {  // the third plane
-    const int base3 = m < 5 ? H::lin3_off(m) : H::fc3_off(m - 5);
-    return base3 + row * HROW3 + hchunk3(row, s >> 3) + 2 * (s & 7);
-  }
-  const int base = m < 5 ? H::lin_off(m) : H::fc_off(m - 5);
-  return base + row * HROW + hchunk(row, s >> 3, plane) + 2 * (s & 7);
-}
-
+// Split-f16 forward weight image (NetH, nc_device.h), prebuilt in global memory by the
+// kernel before k_mlp_fwd (nc_wimage.h) and copied flat into LDS; its builders' range
+// flags fold into amax (the max |w| of the split weights).
 template <int KIND, int NT>
-__device__ __forceinline__ void load_weights_h(char* lds, const nc_decoder_params& P, float& amax) {
-  using N = Net<KIND>;
+__device__ __forceinline__ void copy_wimage(char* lds, const char* img, float& amax) {
   using H = NetH<KIND>;
-  constexpr int CDW = N::XYZ ? HID * N::CD : 1, CB = N::XYZ ? HID : 1, NB = N::XYZ ? 3 * EMB : 1;
-  SegRegs<HID * N::in_real(0), NT> w0;
-  SegRegs<HID * N::in_real(1), NT> w1;
-  SegRegs<HID * N::in_real(2), NT> w2;
-  SegRegs<HID * N::in_real(3), NT> w3;
-  SegRegs<HID * N::in_real(4), NT> w4;
-  SegRegs<5 * HID, NT> bl;
-  SegRegs<CDW, NT> c0, c1, c2, c3, c4;
-  SegRegs<5 * CB, NT> bc;
-  SegRegs<NB, NT> fb;
-  SegRegs<N::NOUT * HID + N::NOUT, NT> ow;
-  w0.load(P.lin_w[0]); w1.load(P.lin_w[1]); w2.load(P.lin_w[2]); w3.load(P.lin_w[3]); w4.load(P.lin_w[4]);
+  const float4* src = reinterpret_cast<const float4*>(img);
+  for (int e = threadIdx.x; e < H::BYTES / 16; e += NT) reinterpret_cast<float4*>(lds)[e] = src[e];
+  const uint32_t* fl = reinterpret_cast<const uint32_t*>(img + H::BYTES);
+  uint32_t f = 0u;
 #pragma unroll
-  for (int k = 0; k < bl.PER; ++k) {
-    const int e = (int)threadIdx.x + k * NT;
-    const int L = e >> 5;
-    const float* b = L == 0 ? P.lin_b[0] : L == 1 ? P.lin_b[1] : L == 2 ? P.lin_b[2] : L == 3 ? P.lin_b[3] : P.lin_b[4];
-    bl.v[k] = (e < 5 * HID) ? b[e & 31] : 0.f;
-  }
-  if constexpr (N::XYZ) {
-    c0.load(P.fc_w[0]); c1.load(P.fc_w[1]); c2.load(P.fc_w[2]); c3.load(P.fc_w[3]); c4.load(P.fc_w[4]);
-#pragma unroll
-    for (int k = 0; k < bc.PER; ++k) {
-      const int e = (int)threadIdx.x + k * NT;
-      const int L = e >> 5;
-      const float* b = L == 0 ? P.fc_b[0] : L == 1 ? P.fc_b[1] : L == 2 ? P.fc_b[2] : L == 3 ? P.fc_b[3] : P.fc_b[4];
-      bc.v[k] = (e < 5 * HID) ? b[e & 31] : 0.f;
-    }
-    fb.load(P.fourier_B);
-  }
-#pragma unroll
-  for (int k = 0; k < ow.PER; ++k) {
-    const int e = (int)threadIdx.x + k * NT;
-    ow.v[k] = (e < N::NOUT * HID) ? P.out_w[e] : (e < N::NOUT * HID + N::NOUT ? P.out_b[e - N::NOUT * HID] : 0.f);
-  }
-  for (int e = threadIdx.x; e < H::BYTES / 16; e += NT) reinterpret_cast<float4*>(lds)[e] = float4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-  float* F = reinterpret_cast<float*>(lds);
-  auto mat = [&](auto& regs, int m, int in, bool lin) {
-#pragma unroll
-    for (int k = 0; k < regs.PER; ++k) {
-      const int e = (int)threadIdx.x + k * NT;
-      if (e < HID * in) {
-        const int o = e / in, c = e - o * in, cp = lin ? N::pack_col(m, c) : c;
-        const float v = regs.v[k];
-        amax = fmaxf(amax, fabsf(v));    // split-f16 range guard (RANGE_LIMIT)
-        // three round-to-nearest planes: v = h + 2^-11 (md + l3) (the residuals are exact in
-        // f32: Sterbenz, then a power-of-two scaling); l3 = r1 - md lies in the f16 subnormal
-        // range for small weights, where its 2^-24 spacing is 2^-35 of the weight's scale:
-        // v is represented to within 3e-11 absolute, below float32's own rounding for |v| > 1e-3
-        const _Float16 h = (_Float16)v;
-        const float r1 = (v - (float)h) * SPLIT_SCALE;
-        const _Float16 md = (_Float16)r1;
-        const _Float16 l3 = (_Float16)(r1 - (float)md);
-        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 0)) = h;
-        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 1)) = md;
-        *reinterpret_cast<_Float16*>(lds + hpos<KIND>(m, o, cp, 2)) = l3;
-      }
-    }
-  };
-  mat(w0, 0, N::in_real(0), true); mat(w1, 1, N::in_real(1), true); mat(w2, 2, N::in_real(2), true);
-  mat(w3, 3, N::in_real(3), true); mat(w4, 4, N::in_real(4), true);
-  bl.store(F, [](int e) { return H::BL + e; });
-  if constexpr (N::XYZ) {
-    mat(c0, 5, N::CD, false); mat(c1, 6, N::CD, false); mat(c2, 7, N::CD, false);
-    mat(c3, 8, N::CD, false); mat(c4, 9, N::CD, false);
-    bc.store(F, [](int e) { return H::BC + e; });
-    fb.store(F, [](int e) {
-      const int k = e / EMB, m = e - k * EMB;
-      return H::FB + k * EMBP + m;
-    });
-  }
-  ow.store(F, [](int e) { return e < N::NOUT * HID ? H::WO + e : H::BO + (e - N::NOUT * HID); });
+  for (int k = 0; k < WIMG_WGS; ++k) f |= fl[k];
+  if (f) amax = __builtin_inff();
   __syncthreads();
 }
 
@@ -684,7 +606,7 @@ __device__ __forceinline__ void fwd_job(const MlpCtx& ctx, const Job& job, int j
   if constexpr (F32)
     load_weights<KIND, PADW_FWD, fwd_threads(FUSE)>(lds, ctx.dec[KIND]);
   else
-    load_weights_h<KIND, fwd_threads(FUSE)>(reinterpret_cast<char*>(lds), ctx.dec[KIND], amax);
+    copy_wimage<KIND, fwd_threads(FUSE)>(reinterpret_cast<char*>(lds), ctx.wimg + (int64_t)j * WIMG_STRIDE, amax);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const int waves = blockDim.x >> 6;
   const int64_t per = 16 * waves * T;  // points per workgroup iteration

@@ -18,6 +18,7 @@
 
 #include "nc_device.h"
 #include "nc_internal.h"
+#include "nc_wimage.h"
 
 namespace nc {
 
@@ -51,8 +52,18 @@ __device__ __forceinline__ bool gt_nan_last(double a, double b) {  // a > b, NaN
 __device__ __forceinline__ double max_nan(double a, double b) { return (a > b || isnan(a)) ? a : b; }
 __device__ __forceinline__ double min_nan(double a, double b) { return (a < b || isnan(a)) ? a : b; }
 
-__global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
+// ray_fill_wgs(c): the fill workgroups after the ray workgroups; then wi.n_jobs * WIMG_WGS
+// workgroups that build k_mlp_fwd's weight images (nc_wimage.h)
+__host__ __device__ inline unsigned ray_fill_wgs(const RayCtx& c) {
+  return (c.zero_fill && c.zero_lo4 > 0) ? (unsigned)c.zero_wgs_setup : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c, const WImgCtx wi) {
   const unsigned nb = (unsigned)((c.N + RAY_WAVES - 1) / RAY_WAVES);  // ray workgroups
+  if (blockIdx.x >= nb + ray_fill_wgs(c)) {
+    wimg_block(wi, (int)(blockIdx.x - nb - ray_fill_wgs(c)));
+    return;
+  }
   if (blockIdx.x >= nb) {  // the first part of the gradient buffer's zero fill (RayCtx::zero_lo4)
     const int64_t nthr = (int64_t)c.zero_wgs_setup * blockDim.x;
     for (int64_t z = (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x; z < c.zero_lo4; z += nthr)
@@ -202,7 +213,12 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c) {
 }
 
 // points mode (NICE.forward on caller points): the same per-point prologue
-__global__ void k_points_prep(const MlpCtx m, float4* xyz, float4* pf) {
+__global__ void __launch_bounds__(256) k_points_prep(const MlpCtx m, const WImgCtx wi, float4* xyz, float4* pf) {
+  const unsigned nb = (unsigned)((m.P + 255) / 256);
+  if (blockIdx.x >= nb) {  // k_mlp_fwd's weight images (nc_wimage.h)
+    wimg_block(wi, (int)(blockIdx.x - nb));
+    return;
+  }
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p < MAX_JOBS && m.range_flag) m.range_flag[p] = 0u;  // for k_mlp_fwd
   if (p >= m.P) return;
@@ -874,9 +890,9 @@ int launch_depth_max(const float* gt, const uint8_t* valid, int64_t n, float* ou
   hipLaunchKernelGGL(k_depth_max, dim3(1), dim3(1024), 0, s, gt, valid, n, out);
   return (int)hipGetLastError();
 }
-int launch_ray_setup(const RayCtx& c, hipStream_t s) {
-  hipLaunchKernelGGL(k_ray_setup, dim3(ray_blocks(c.N) + (c.zero_fill && c.zero_lo4 > 0 ? (unsigned)c.zero_wgs_setup : 0u)),
-                     dim3(256), 0, s, c);
+int launch_ray_setup(const RayCtx& c, const WImgCtx& wi, hipStream_t s) {
+  hipLaunchKernelGGL(k_ray_setup, dim3(ray_blocks(c.N) + ray_fill_wgs(c) + (unsigned)(wi.n_jobs * WIMG_WGS)),
+                     dim3(256), 0, s, c, wi);
   return (int)hipGetLastError();
 }
 int launch_composite_fwd(const RayCtx& c, hipStream_t s) {
@@ -924,8 +940,9 @@ int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, flo
                      g_raw, gocc, grgb);
   return (int)hipGetLastError();
 }
-int launch_points_prep(const MlpCtx& m, float4* xyz, float4* pf, hipStream_t s) {
-  hipLaunchKernelGGL(k_points_prep, dim3((unsigned)((m.P + 255) / 256)), dim3(256), 0, s, m, xyz, pf);
+int launch_points_prep(const MlpCtx& m, const WImgCtx& wi, float4* xyz, float4* pf, hipStream_t s) {
+  hipLaunchKernelGGL(k_points_prep, dim3((unsigned)((m.P + 255) / 256) + (unsigned)(wi.n_jobs * WIMG_WGS)), dim3(256), 0,
+                     s, m, wi, xyz, pf);
   return (int)hipGetLastError();
 }
 int launch_points_grads(const MlpCtx& m, double* g_pts, hipStream_t s) {

@@ -83,12 +83,6 @@ PATCHES = {
         ("nc_mlp.hip", "      wave_forward_h<KIND, T>(reinterpret_cast<const char*>(lds), i, g, R, out, rec, job.keep_h != 0, amax);",
          "      { for (int t = 0; t < T; ++t) for (int o = 0; o < 4; ++o) out[t][o] = R[t].c[o]; }"),
     ],
-    "fwd_no_wimage": [  # k_mlp_fwd: no weight image (garbage LDS weights; range guard held off)
-        ("nc_mlp.hip", "    load_weights_h<KIND, fwd_threads(FUSE)>(reinterpret_cast<char*>(lds), ctx.dec[KIND], amax);",
-         "    __syncthreads();"),
-        ("nc_mlp.hip", "    if (!(amax < RANGE_LIMIT) && ctx.range_flag) ctx.range_flag[j] = 1u;",
-         "    if (amax == -1.f && ctx.range_flag) ctx.range_flag[j] = 1u;"),
-    ],
     "gather_hot": [  # every corner row read from grid row 0 (one line: L1 hits; timing only)
         ("nc_device.h", "  return ((c.inb >> k) & 1u) ? G.data + (c.base + corner_delta(G.stride, k)) : kZeroRow;",
          "  return ((c.inb >> k) & 1u) ? G.data : kZeroRow;"),
@@ -100,6 +94,10 @@ PATCHES = {
     "gather_8mb": [  # corner rows folded into the grid's first 8 MiB (timing only)
         ("nc_device.h", "  return ((c.inb >> k) & 1u) ? G.data + (c.base + corner_delta(G.stride, k)) : kZeroRow;",
          "  return ((c.inb >> k) & 1u) ? G.data + ((c.base + corner_delta(G.stride, k)) & 0x1fffe0) : kZeroRow;"),
+    ],
+    "dx_no_wimage": [  # k_mlp_dx: no f32 weight image (garbage LDS weights; timing only): the
+        # prologue's share, i.e. what a prebuilt image (nc_wimage.h for the forward) could save
+        ("nc_mlp.hip", "  load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);", "  __syncthreads();"),
     ],
     "swz3_old": [  # the round-5 third-plane swizzle (2-way LDS bank conflicts on its reads; results valid)
         ("nc_device.h", "return 16 * (g ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3));", "return 16 * (g ^ ((row >> 2) & 3));"),
