@@ -225,7 +225,7 @@ int check_models(const Plan& pl, const nc_grid* grids, const nc_decoder_params* 
 }
 
 struct Ws {
-  size_t dmax = 0, rflag = 0, wimg = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
+  size_t dmax = 0, rflag = 0, wimg = 0, dximg = 0, z = 0, pts = 0, xyz = 0, pf = 0, occ = 0, rgb = 0, gocc = 0, grgb = 0, dpts = 0, slab = 0, rec = 0, feat = 0,
          gocc_b = 0, grgb_b = 0,  // fused mapper loss: d raw of a backward that is not d loss alone
          lpart = 0, lcount = 0,   // fused mapper loss: per-workgroup partial sums + done counter
          coef_d = 0, coef_c = 0, bslab = 0, dfeat = 0, dkey[2] = {0, 0}, dval[2] = {0, 0}, dw = 0, dpart = 0, dtemp = 0,
@@ -327,6 +327,7 @@ void layout(int64_t N, int64_t P, const Plan& pl, bool rays, bool save, bool los
     w.lcount = take(16);
   }
   w.save = save;
+  w.dximg = save ? take((size_t)pl.n_jobs * DXIMG_STRIDE) : 0;  // MlpCtx::dximg (k_mlp_dx's weights)
   // the fused gather (k_mlp_fwd) cannot claim sparse rows or save the Jacobian
   w.fuse = fuse && !w.claims && !w.has_jac;
   if (save) {
@@ -453,6 +454,7 @@ void fill_mlp(MlpCtx& m, int64_t P, const Plan& pl, const nc_grid* grids, const 
   m.dfeat = w.det ? at<float>(ws, w.dfeat) : nullptr;
   m.range_flag = at<uint32_t>(ws, w.rflag);
   m.wimg = at<char>(ws, w.wimg);
+  m.dximg = w.save ? at<float>(ws, w.dximg) : nullptr;
   m.bslab = w.save ? at<float>(ws, w.bslab) : nullptr;
   m.bslab_rows = w.bslab_rows;
   m.jac = w.has_jac ? at<float>(ws, w.jac) : nullptr;
@@ -464,6 +466,8 @@ static WImgCtx wimg_ctx(const MlpCtx& m) {
   std::memset(&wi, 0, sizeof(wi));
   wi.n_jobs = m.n_jobs;
   wi.img = const_cast<char*>(m.wimg);
+  wi.dximg = const_cast<float*>(m.dximg);  // a forward for a backward: k_mlp_dx's image too
+  wi.wgs_per_job = WIMG_WGS * (m.dximg ? 2 : 1);
   for (int j = 0; j < m.n_jobs; ++j) {
     wi.kind[j] = m.jobs[j].kind;
     wi.dec[j] = m.dec[m.jobs[j].kind];

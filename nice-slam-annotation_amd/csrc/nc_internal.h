@@ -33,7 +33,9 @@ static_assert(CLAIM_SHARDS <= 64, "k_rows_compact sums the shard counters across
 struct WImgCtx {
   int32_t n_jobs;      // 0: no builder workgroups
   int32_t kind[MAX_JOBS];
+  int32_t wgs_per_job; // WIMG_WGS (forward image) + WIMG_WGS when dximg is set
   char* img;           // [n_jobs][WIMG_STRIDE] (MlpCtx::wimg)
+  float* dximg;        // [n_jobs][DXIMG_STRIDE / 4] k_mlp_dx's f32 image (MlpCtx::dximg), or NULL
   nc_decoder_params dec[MAX_JOBS];
 };
 
@@ -84,6 +86,8 @@ struct MlpCtx {
                              // mapper loss, RayCtx::fuse_bwd), or NULL
   const char* wimg;          // [n_jobs][WIMG_STRIDE] split-f16 weight images + flag words (nc_wimage.h),
                              // built by the kernel before k_mlp_fwd (WImgCtx)
+  const float* dximg;        // [n_jobs][DXIMG_STRIDE / 4] k_mlp_dx's f32 weight images (Net<KIND, PADW_BWD>),
+                             // built with wimg by a forward that saves for the backward
   uint32_t* range_flag;      // [MAX_JOBS] split-f16 range guard: k_mlp_fwd sets job j's word when
                              // an operand reached RANGE_LIMIT, k_mlp_fwd_exact then recomputes the
                              // job in f32; zeroed by k_ray_setup / k_points_prep (NULL: no guard)

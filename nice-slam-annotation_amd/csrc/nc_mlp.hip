@@ -811,8 +811,12 @@ __device__ __forceinline__ void dx_job(const MlpCtx& ctx, const Job& job, float*
   const bool need_coord = job.need_coord != 0;
   const bool need_dc = need_grid || need_coord;
   float* bacc = lds + DX_BACC + wave * DX_BSLAB;  // this wave's d fourier_B (xyz decoders, weight gradients)
-  for (int e = threadIdx.x; e < waves * DX_BSLAB; e += blockDim.x) lds[DX_BACC + e] = 0.f;  // ordered by load_weights' barrier
-  load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);
+  for (int e = threadIdx.x; e < waves * DX_BSLAB; e += blockDim.x) lds[DX_BACC + e] = 0.f;  // ordered by the image copy's barrier
+  {  // the f32 image the forward's builders wrote (nc_wimage.h dximg_build), copied flat
+    const float4* src = reinterpret_cast<const float4*>(ctx.dximg + (int64_t)blockIdx.y * (DXIMG_STRIDE / 4));
+    for (int e = threadIdx.x; e < Net<KIND, PADW_BWD>::WEIGHTS / 4; e += DX_THREADS) reinterpret_cast<float4*>(lds)[e] = src[e];
+    __syncthreads();
+  }
   // this wave's scatter staging (a scalar base: nothing per lane to keep live across tiles)
   float* slice = lds + DX_SLICE_BASE + __builtin_amdgcn_readfirstlane(wave) * SCAT_FLOATS;
   const int64_t ntiles = (ctx.P + 15) / 16;

@@ -891,7 +891,7 @@ int launch_depth_max(const float* gt, const uint8_t* valid, int64_t n, float* ou
   return (int)hipGetLastError();
 }
 int launch_ray_setup(const RayCtx& c, const WImgCtx& wi, hipStream_t s) {
-  hipLaunchKernelGGL(k_ray_setup, dim3(ray_blocks(c.N) + ray_fill_wgs(c) + (unsigned)(wi.n_jobs * WIMG_WGS)),
+  hipLaunchKernelGGL(k_ray_setup, dim3(ray_blocks(c.N) + ray_fill_wgs(c) + (unsigned)(wi.n_jobs * wi.wgs_per_job)),
                      dim3(256), 0, s, c, wi);
   return (int)hipGetLastError();
 }
@@ -941,7 +941,7 @@ int launch_points_split_grad(const MlpCtx& m, int stage, const float* g_raw, flo
   return (int)hipGetLastError();
 }
 int launch_points_prep(const MlpCtx& m, const WImgCtx& wi, float4* xyz, float4* pf, hipStream_t s) {
-  hipLaunchKernelGGL(k_points_prep, dim3((unsigned)((m.P + 255) / 256) + (unsigned)(wi.n_jobs * WIMG_WGS)), dim3(256), 0,
+  hipLaunchKernelGGL(k_points_prep, dim3((unsigned)((m.P + 255) / 256) + (unsigned)(wi.n_jobs * wi.wgs_per_job)), dim3(256), 0,
                      s, m, wi, xyz, pf);
   return (int)hipGetLastError();
 }

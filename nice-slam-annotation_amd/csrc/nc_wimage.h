@@ -139,9 +139,63 @@ __device__ __forceinline__ void wimg_build(const WSrc& P, char* img, int slice) 
   if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(img + H::BYTES)[slice] = flag ? 1u : 0u;
 }
 
-// builder workgroup b (0 .. n_jobs * WIMG_WGS) of a kernel's extra workgroups
+// k_mlp_dx's f32 image (Net<KIND, PADW_BWD>: what load_weights<KIND, PADW_BWD> writes
+// into LDS), built by the same forward (the backward reads the weights the forward used,
+// as the reference's saved tensors): float4 items, region by region (each region's
+// pointer a constant), padding columns written as zeros.  The tail (biases, output
+// layer, Fourier B) has the f32-part layout of the split image, at N::BL.
+constexpr int DXIMG_FLOATS = wimg_max(wimg_max(Net<K_COARSE, PADW_BWD>::WEIGHTS, Net<K_MID, PADW_BWD>::WEIGHTS),
+                                      wimg_max(Net<K_FINE, PADW_BWD>::WEIGHTS, Net<K_COLOR, PADW_BWD>::WEIGHTS));
+constexpr int64_t DXIMG_STRIDE = ((int64_t)DXIMG_FLOATS * 4 + 255) & ~int64_t(255);
+
+template <int KIND>
+__device__ __forceinline__ void dximg_build(const WSrc& P, float* img, int slice) {
+  using N = Net<KIND, PADW_BWD>;
+  constexpr int STRIDE = WIMG_WGS * WIMG_THREADS;
+  constexpr int NMAT = N::XYZ ? 10 : 5;
+  const int gt = slice * WIMG_THREADS + (int)threadIdx.x;
+  int base = 0;  // item (float4) number of the region's first item
+#pragma unroll
+  for (int m = 0; m < NMAT; ++m) {
+    const int ld = m < 5 ? N::lin_ld(m) : N::LDC;
+    const int off = m < 5 ? N::lin_off(m) : N::WC + (m - 5) * HID * N::LDC;
+    const int n4 = HID * ld / 4;
+    const float* W = m == 0 ? P.lin_w[0] : m == 1 ? P.lin_w[1] : m == 2 ? P.lin_w[2] : m == 3 ? P.lin_w[3]
+                   : m == 4 ? P.lin_w[4] : m == 5 ? P.fc_w[0] : m == 6 ? P.fc_w[1] : m == 7 ? P.fc_w[2]
+                   : m == 8 ? P.fc_w[3] : P.fc_w[4];
+    for (int it = base + (((gt - base) % STRIDE) + STRIDE) % STRIDE; it < base + n4; it += STRIDE) {
+      const int e = 4 * (it - base), o = e / ld, c0 = e - o * ld;
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c0 + k;
+        if (m < 5) {
+          const int rc = c < (m == 0 ? N::IN0 : m == 3 ? N::IN3 : HID) ? N::real_col(m, c) : -1;
+          v[k] = rc >= 0 ? W[o * N::in_real(m) + rc] : 0.f;
+        } else {
+          v[k] = c < N::CD ? W[o * N::CD + c] : 0.f;
+        }
+      }
+      reinterpret_cast<float4*>(img + off)[it - base] = float4{v[0], v[1], v[2], v[3]};
+    }
+    base += n4;
+  }
+  // the tail [BL, WEIGHTS): N::BL is a multiple of 4 floats
+  constexpr int T4 = (N::WEIGHTS - N::BL) / 4;
+  for (int it = base + (((gt - base) % STRIDE) + STRIDE) % STRIDE; it < base + T4; it += STRIDE) {
+    const int e = 4 * (it - base);
+    float4 v;
+    v.x = wimg_f32<KIND>(P, e + 0);
+    v.y = wimg_f32<KIND>(P, e + 1);
+    v.z = wimg_f32<KIND>(P, e + 2);
+    v.w = wimg_f32<KIND>(P, e + 3);
+    reinterpret_cast<float4*>(img + N::BL)[e / 4] = v;
+  }
+}
+
+// builder workgroup b (0 .. n_jobs * wgs_per_job) of a kernel's extra workgroups
 __device__ __forceinline__ void wimg_block(const WImgCtx& w, int b) {
-  const int j = b / WIMG_WGS, slice = b - j * WIMG_WGS;
+  const int j = b / w.wgs_per_job, slice = b - j * w.wgs_per_job;
   if (j >= w.n_jobs) return;
   const int kind = j == 0 ? w.kind[0] : (j == 1 ? w.kind[1] : w.kind[2]);
   auto sel = [j](const float* a, const float* b, const float* c) { return j == 0 ? a : (j == 1 ? b : c); };
@@ -156,6 +210,16 @@ __device__ __forceinline__ void wimg_block(const WImgCtx& w, int b) {
   P.fourier_B = sel(w.dec[0].fourier_B, w.dec[1].fourier_B, w.dec[2].fourier_B);
   P.out_w = sel(w.dec[0].out_w, w.dec[1].out_w, w.dec[2].out_w);
   P.out_b = sel(w.dec[0].out_b, w.dec[1].out_b, w.dec[2].out_b);
+  if (slice >= WIMG_WGS) {  // k_mlp_dx's f32 image
+    float* dimg = w.dximg + (int64_t)j * (DXIMG_STRIDE / 4);
+    switch (kind) {
+      case K_COARSE: dximg_build<K_COARSE>(P, dimg, slice - WIMG_WGS); break;
+      case K_MID: dximg_build<K_MID>(P, dimg, slice - WIMG_WGS); break;
+      case K_FINE: dximg_build<K_FINE>(P, dimg, slice - WIMG_WGS); break;
+      default: dximg_build<K_COLOR>(P, dimg, slice - WIMG_WGS); break;
+    }
+    return;
+  }
   char* img = w.img + (int64_t)j * WIMG_STRIDE;
   switch (kind) {
     case K_COARSE: wimg_build<K_COARSE>(P, img, slice); break;

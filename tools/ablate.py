@@ -95,9 +95,10 @@ PATCHES = {
         ("nc_device.h", "  return ((c.inb >> k) & 1u) ? G.data + (c.base + corner_delta(G.stride, k)) : kZeroRow;",
          "  return ((c.inb >> k) & 1u) ? G.data + ((c.base + corner_delta(G.stride, k)) & 0x1fffe0) : kZeroRow;"),
     ],
-    "dx_no_wimage": [  # k_mlp_dx: no f32 weight image (garbage LDS weights; timing only): the
-        # prologue's share, i.e. what a prebuilt image (nc_wimage.h for the forward) could save
-        ("nc_mlp.hip", "  load_weights<KIND, PADW_BWD, DX_THREADS>(lds, ctx.dec[KIND]);", "  __syncthreads();"),
+    "dx_no_wimage": [  # k_mlp_dx: no copy of its prebuilt f32 weight image (garbage LDS weights;
+        # timing only): the prologue's remaining share
+        ("nc_mlp.hip", "    for (int e = threadIdx.x; e < Net<KIND, PADW_BWD>::WEIGHTS / 4; e += DX_THREADS) "
+                       "reinterpret_cast<float4*>(lds)[e] = src[e];", "    (void)src;"),
     ],
     "swz3_old": [  # the round-5 third-plane swizzle (2-way LDS bank conflicts on its reads; results valid)
         ("nc_device.h", "return 16 * (g ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3));", "return 16 * (g ^ ((row >> 2) & 3));"),
