@@ -524,6 +524,21 @@ def _attach(pairs):
             p.grad.add_(g)
 
 
+def _versions(params):
+    return tuple(p._version if isinstance(p, torch.Tensor) else None for p in params)
+
+
+def _check_versions(params, versions):
+    """The backward reads the decoder weights the forward used (k_mlp_dx's weight image is
+    built by the forward, nc_wimage.h), as the reference's nn.Linear saves its weight for
+    backward: a parameter changed in place in between is an error there, and here."""
+    for p, v in zip(params, versions):
+        if isinstance(p, torch.Tensor) and p._version != v:
+            raise RuntimeError("one of the variables needed for gradient computation has been modified by an "
+                               "inplace operation: a decoder parameter changed between the nicecore forward "
+                               "and its backward")
+
+
 class NiceRenderFn(torch.autograd.Function):
     """render_batch_ray on the HIP core.  Inputs: (spec, rays_o, rays_d, gt_depth|None,
     grid_coarse|None, grid_middle|None, grid_fine|None, grid_color|None, *params).
@@ -644,6 +659,7 @@ class NiceRenderFn(torch.autograd.Function):
         ctx.sparse = sparse
         ctx.defer = spec.get("defer")
         ctx.keep = (rays_o, rays_d, gt, dmax, gkeep, params, tgt, zx, tr, rv)
+        ctx.pversions = _versions(params)
         a.z_out, a.weights_out = None, None  # pass-1 outputs: not rewritten by the backward
         ctx.grids = grids
         if loss is None:
@@ -652,6 +668,7 @@ class NiceRenderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_depth, g_var, g_color, g_loss=None):
+        _check_versions(ctx.keep[5], ctx.pversions)
         lib = L.load()
         a, plan = ctx.args, ctx.plan
         need = ctx.needs_input_grad
@@ -788,12 +805,14 @@ class NiceEvalFn(torch.autograd.Function):
         ctx.args, ctx.ws, ctx.nbytes, ctx.plan = a, ws, nbytes, plan
         ctx.sparse = sparse
         ctx.keep = (pts, gkeep, params)
+        ctx.pversions = _versions(params)
         ctx.grids = grids
         ctx.p_dtype, ctx.p_shape = p.dtype, p.shape
         return raw
 
     @staticmethod
     def backward(ctx, g_raw):
+        _check_versions(ctx.keep[2], ctx.pversions)
         lib = L.load()
         a, plan = ctx.args, ctx.plan
         need = ctx.needs_input_grad

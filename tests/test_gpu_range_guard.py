@@ -60,7 +60,7 @@ def test_points_forward_past_f16_range(what, scale, stage):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("what,scale", [("grid", 2.0e5), ("bias", 1.0e5)])
+@pytest.mark.parametrize("what,scale", [("grid", 2.0e5), ("bias", 1.0e5), ("weight", 7.0e4)])
 def test_render_past_f16_range_with_gradients(what, scale):
     """render_batch_ray + backward: the backward reads the activation records the exact
     recompute wrote (relu masks, h_L), so its gradients are the f32 path's."""
