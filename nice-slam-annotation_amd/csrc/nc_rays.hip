@@ -52,28 +52,31 @@ __device__ __forceinline__ bool gt_nan_last(double a, double b) {  // a > b, NaN
 __device__ __forceinline__ double max_nan(double a, double b) { return (a > b || isnan(a)) ? a : b; }
 __device__ __forceinline__ double min_nan(double a, double b) { return (a < b || isnan(a)) ? a : b; }
 
-// ray_fill_wgs(c): the fill workgroups after the ray workgroups; then wi.n_jobs * WIMG_WGS
-// workgroups that build k_mlp_fwd's weight images (nc_wimage.h)
+// grid: wi.n_jobs * wi.wgs_per_job workgroups that build the decoders' weight images
+// (nc_wimage.h), the ray workgroups, then ray_fill_wgs(c) fill workgroups
 __host__ __device__ inline unsigned ray_fill_wgs(const RayCtx& c) {
   return (c.zero_fill && c.zero_lo4 > 0) ? (unsigned)c.zero_wgs_setup : 0u;
 }
 
 __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c, const WImgCtx wi) {
-  const unsigned nb = (unsigned)((c.N + RAY_WAVES - 1) / RAY_WAVES);  // ray workgroups
-  if (blockIdx.x >= nb + ray_fill_wgs(c)) {
-    wimg_block(wi, (int)(blockIdx.x - nb - ray_fill_wgs(c)));
+  // the weight-image builders first (dispatched with the rays, not after the fill)
+  const unsigned nbuild = (unsigned)(wi.n_jobs * wi.wgs_per_job);
+  if (blockIdx.x < nbuild) {
+    wimg_block(wi, (int)blockIdx.x);
     return;
   }
-  if (blockIdx.x >= nb) {  // the first part of the gradient buffer's zero fill (RayCtx::zero_lo4)
+  const unsigned blk = blockIdx.x - nbuild;
+  const unsigned nb = (unsigned)((c.N + RAY_WAVES - 1) / RAY_WAVES);  // ray workgroups
+  if (blk >= nb) {  // the first part of the gradient buffer's zero fill (RayCtx::zero_lo4)
     const int64_t nthr = (int64_t)c.zero_wgs_setup * blockDim.x;
-    for (int64_t z = (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x; z < c.zero_lo4; z += nthr)
+    for (int64_t z = (int64_t)(blk - nb) * blockDim.x + threadIdx.x; z < c.zero_lo4; z += nthr)
       c.zero_fill[z] = float4{0.f, 0.f, 0.f, 0.f};
     return;
   }
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * RAY_WAVES + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x < MAX_JOBS && c.range_flag) c.range_flag[threadIdx.x] = 0u;  // for k_mlp_fwd
-  if (blockIdx.x == 0 && threadIdx.x == 0 && c.fuse_bwd) *c.loss_count = 0u;  // k_composite_fwd_loss's done counter
+  const int64_t r = (int64_t)blk * RAY_WAVES + (threadIdx.x >> 6);
+  if (blk == 0 && threadIdx.x < MAX_JOBS && c.range_flag) c.range_flag[threadIdx.x] = 0u;  // for k_mlp_fwd
+  if (blk == 0 && threadIdx.x == 0 && c.fuse_bwd) *c.loss_count = 0u;  // k_composite_fwd_loss's done counter
   // this ray's inputs first: their loads overlap the batch-max loop below
   const bool live = r < c.N;
   const int64_t rr = live ? r : 0;
@@ -214,12 +217,12 @@ __global__ void __launch_bounds__(256) k_ray_setup(const RayCtx c, const WImgCtx
 
 // points mode (NICE.forward on caller points): the same per-point prologue
 __global__ void __launch_bounds__(256) k_points_prep(const MlpCtx m, const WImgCtx wi, float4* xyz, float4* pf) {
-  const unsigned nb = (unsigned)((m.P + 255) / 256);
-  if (blockIdx.x >= nb) {  // k_mlp_fwd's weight images (nc_wimage.h)
-    wimg_block(wi, (int)(blockIdx.x - nb));
+  const unsigned nbuild = (unsigned)(wi.n_jobs * wi.wgs_per_job);
+  if (blockIdx.x < nbuild) {  // the decoders' weight images (nc_wimage.h)
+    wimg_block(wi, (int)blockIdx.x);
     return;
   }
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = (int64_t)(blockIdx.x - nbuild) * blockDim.x + threadIdx.x;
   if (p < MAX_JOBS && m.range_flag) m.range_flag[p] = 0u;  // for k_mlp_fwd
   if (p >= m.P) return;
   double pt[3];

@@ -21,7 +21,10 @@
 
 namespace nc {
 
-constexpr int WIMG_WGS = 8;        // builder workgroups per job (256 threads each)
+#ifndef NC_WIMG_WGS
+#define NC_WIMG_WGS 8
+#endif
+constexpr int WIMG_WGS = NC_WIMG_WGS;  // builder workgroups per job and image (256 threads each)
 constexpr int WIMG_THREADS = 256;
 
 template <int KIND>

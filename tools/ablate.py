@@ -100,6 +100,14 @@ PATCHES = {
         ("nc_mlp.hip", "    for (int e = threadIdx.x; e < Net<KIND, PADW_BWD>::WEIGHTS / 4; e += DX_THREADS) "
                        "reinterpret_cast<float4*>(lds)[e] = src[e];", "    (void)src;"),
     ],
+    "wimg_last": [  # k_ray_setup: the weight-image builders after the ray and fill workgroups (round 6's first form)
+        ("nc_rays.hip", "  if (blockIdx.x < nbuild) {\n    wimg_block(wi, (int)blockIdx.x);\n    return;\n  }\n"
+                        "  const unsigned blk = blockIdx.x - nbuild;\n"
+                        "  const unsigned nb = (unsigned)((c.N + RAY_WAVES - 1) / RAY_WAVES);  // ray workgroups\n",
+         "  const unsigned nb = (unsigned)((c.N + RAY_WAVES - 1) / RAY_WAVES);  // ray workgroups\n"
+         "  if (blockIdx.x >= nb + ray_fill_wgs(c)) {\n    wimg_block(wi, (int)(blockIdx.x - nb - ray_fill_wgs(c)));\n"
+         "    return;\n  }\n  const unsigned blk = blockIdx.x;\n  (void)nbuild;\n"),
+    ],
     "swz3_old": [  # the round-5 third-plane swizzle (2-way LDS bank conflicts on its reads; results valid)
         ("nc_device.h", "return 16 * (g ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3));", "return 16 * (g ^ ((row >> 2) & 3));"),
     ],
@@ -113,6 +121,8 @@ PATCHES["dx_no_trilinear"] = PATCHES["dx_no_scatter"] + PATCHES["dx_no_coord"]
 DEFINES = {
     "ref": [],
     "mfma_f32": ["-DNC_MFMA_F32"],  # the exact-f32 MFMA forward (a numerics A/B, results valid)
+    "wimg4": ["-DNC_WIMG_WGS=4"],  # weight-image builder workgroups per decoder and image
+    "wimg16": ["-DNC_WIMG_WGS=16"],
     "dx512": ["-DNC_DX_THREADS=512"],
     "dx1024": ["-DNC_DX_THREADS=1024"],  # 16 waves: 4 per SIMD at <= 128 VGPRs
     "dw512_16": ["-DNC_DW_THREADS=512", "-DNC_DW_NPTS=16"],
