@@ -108,6 +108,14 @@ PATCHES = {
          "  if (blockIdx.x >= nb + ray_fill_wgs(c)) {\n    wimg_block(wi, (int)(blockIdx.x - nb - ray_fill_wgs(c)));\n"
          "    return;\n  }\n  const unsigned blk = blockIdx.x;\n  (void)nbuild;\n"),
     ],
+    "exact_nolds": [  # k_mlp_fwd_exact (the range guard's no-op pass) launched without its dynamic LDS
+        # (timing only: a flagged job would fault; never flagged at C2): what the LDS request costs
+        ("nc_mlp.hip", "    hipLaunchKernelGGL(k_mlp_fwd_exact<true>, xgrid, dim3(FWD_THREADS_FUSED), mlp_fwd_exact_lds_bytes(), s, x);",
+         "    hipLaunchKernelGGL(k_mlp_fwd_exact<true>, xgrid, dim3(FWD_THREADS_FUSED), 0, s, x);"),
+    ],
+    "no_exact": [  # no k_mlp_fwd_exact launch at all (timing only): the guard pass's whole cost in the step
+        ("nc_mlp.hip", "  if (FWD_F32 || c.range_flag == nullptr) return 0;", "  return 0;"),
+    ],
     "swz3_old": [  # the round-5 third-plane swizzle (2-way LDS bank conflicts on its reads; results valid)
         ("nc_device.h", "return 16 * (g ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3));", "return 16 * (g ^ ((row >> 2) & 3));"),
     ],
