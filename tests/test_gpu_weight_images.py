@@ -55,3 +55,39 @@ def test_images_rebuilt_per_forward():
         b = model(pts, g, "color")
     assert torch.allclose(b[:, :3], a[:, :3] + 1.0, atol=1e-5)
     assert torch.equal(b[:, 3], a[:, 3])
+
+
+def _run_all(model, g, rec, bound):
+    ro, rd = rec["rays_o"].cuda().requires_grad_(True), rec["rays_d"].cuda().requires_grad_(True)
+    for p in model.parameters():
+        p.grad = None
+    d, v, c = make_renderer(bound).render_batch_ray(g, model, rd, ro, "cuda", "color", rec["gt_depth"].cuda())
+    (d.sum() + v.sum() + c.sum()).backward()
+    out = {"depth": d.detach(), "var": v.detach(), "color": c.detach(), "g_ro": ro.grad, "g_rd": rd.grad}
+    out.update({"p/" + n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+    with torch.no_grad():
+        out["raw"] = model(rec["pts"].cuda(), g, "color")
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.gpu
+def test_images_cover_their_workspace(monkeypatch):
+    """The builders write every 16-B chunk of both images (no zero fill): a workspace whose
+    bytes are all 0xFF (NaN as floats) before the call gives bit-identical outputs and
+    decoder / ray gradients."""
+    bound, rec, model, g = _setup()
+    clean = _run_all(model, g, rec, bound)
+    real_empty = torch.empty
+
+    def poisoned(*a, **kw):
+        t = real_empty(*a, **kw)
+        if kw.get("dtype") is torch.uint8 and t.is_cuda:
+            t.fill_(255)
+        return t
+
+    monkeypatch.setattr(torch, "empty", poisoned)
+    dirty = _run_all(model, g, rec, bound)
+    monkeypatch.setattr(torch, "empty", real_empty)
+    for k, t in clean.items():
+        assert torch.equal(t, dirty[k]), k
